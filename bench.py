@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/s of the per-pixel sample loop (camera::render -> ray_color -> bvh/sphere hit
+-> material::scatter) on the book-1 random-sphere scene, BASELINE config 2: 1920x1080, 500 spp,
+depth 50, on the MI355X kernels of librtgpu.so.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A step renders one full frame: rank r renders rows r, r+N, ... (interleaved tiling) into a
+device buffer and the frame is gathered on rank 0 over RCCL (torch.distributed "nccl"). The scene
+is built and uploaded before timing (reported separately). value = ray segments traced by all
+ranks / max-over-ranks wall time of the K timed steps. Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "raytracing-practice_amd", "python"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+METRIC = "Mrays/sec at 1920×1080, 500 spp, depth 50; per-pixel RMSE vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_BOX, BYTES_PER_PRIM, BYTES_PER_HIT = 32, 32, 16  # SURVEY.md §8d algorithmic bytes
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="bouncing_spheres")
+    ap.add_argument("--grid", type=int, default=11, help="bouncing_spheres grid half-width (500 = 1M spheres)")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--bvh", choices=["sah", "median"], default="sah")
+    ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU sample")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, scene_desc, cam):
+    """The reference timed on this host's cores: oracle/_ref/ref_harness (reference geometry,
+    BVH, RNG and vector code compiled from /root/reference; camera/material loop restated, see
+    DESIGN.md 'ref-hybrid') if it was built, else the oracle's fp64 port (cpu_ref64)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = args.cpu_threads or min(int(os.environ.get("OMP_NUM_THREADS", "16")), avail, 16)
+    W, H, spp, depth = args.width, args.height, args.cpu_spp, args.depth
+    sample = f"{args.scene} {W}x{H}, {spp} spp, depth {depth}, rows dealt over {threads} workers"
+    harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
+    if args.scene == "bouncing_spheres" and args.grid == 11 and os.access(harness, os.X_OK):
+        try:
+            out = subprocess.run([harness, "bench", "book1", str(W), str(H), str(spp), str(depth),
+                                  str(threads)], check=True, capture_output=True, text=True,
+                                 timeout=600).stdout
+            r = json.loads(out)
+            return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads,
+                    "kind": "reference", "sample": sample + " (ref-hybrid build)",
+                    "seconds": round(r["seconds"], 3), "segments": r["segments"]}
+        except (subprocess.SubprocessError, OSError, ValueError, KeyError) as e:
+            print(f"[bench] ref_harness failed ({e}); timing the fp64 port instead", file=sys.stderr)
+    import rtgpu
+    from oracle_bind import Oracle
+
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(cam)
+    c.samples_per_pixel = spp
+    sec, segs = Oracle().bench_f64(scene_desc, c, threads, H)
+    return {"value": round(segs / sec / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": sample + " (cpu_ref64)", "seconds": round(sec, 3), "segments": segs}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per render launch measured by rocprofv3 PMC passes (profiles/pmc_*.json, written by
+    profiles/collect_pmc.py for the same workload); None when no matching measurement exists."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+        if rec.get("workload") == workload:
+            return rec.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import rtgpu
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+
+    lib = rtgpu.Library()
+    scenes = rtgpu.SceneLibrary()
+    bvh = rtgpu.RTG_BVH_SAH if args.bvh == "sah" else rtgpu.RTG_BVH_MEDIAN
+    t0 = time.perf_counter()
+    s = scenes.build(args.scene, grid=args.grid, image_width=args.width,
+                     aspect_ratio=args.width / args.height, spp=args.spp, max_depth=args.depth,
+                     bvh_mode=bvh, rand_seed=1)
+    cam = s.camera
+    t_scene = time.perf_counter() - t0
+    params = lib.camera_resolve(cam)
+    H, W = params.image_height, params.image_width
+    ds = lib.scene_create(s.desc, device=local)
+    info = ds.info()
+    b, stride, n = rtgpu.shard_rows(H, rank, world)
+    shard = torch.zeros((rtgpu.padded_rows(H, world), W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step(i):
+        st = ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + i, row_begin=b,
+                              row_stride=stride, row_count=n)
+        if world > 1:
+            rtgpu.gather_frame(shard, H)
+        return st
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    segs, kernel_ms = 0, []
+    for i in range(args.steps):
+        st = step(args.warmup + i)
+        segs += st.segments
+        kernel_ms.append(st.kernel_ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+
+    tot = torch.tensor([float(segs)], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    total_segs, wall = float(tot.item()), float(tmax.item())
+
+    # algorithmic bytes of one launch (counting variant of the same kernel, same seed, untimed)
+    cst = ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + args.warmup, row_begin=b,
+                           row_stride=stride, row_count=n, count=True)
+    algo_bytes = (BYTES_PER_BOX * cst.box_tests + BYTES_PER_PRIM * cst.prim_tests
+                  + BYTES_PER_HIT * cst.hits)
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    achieved = algo_bytes / avg_kernel_s / 1e9
+    workload = f"{args.scene}(grid={args.grid}) {W}x{H} {args.spp}spp depth{args.depth} bvh={args.bvh}"
+
+    if rank == 0:
+        samples = W * H * args.spp * args.steps
+        line = {
+            "metric": METRIC,
+            "value": round(total_segs / wall / 1e6, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (the reference's book-1 scene regenerated from glibc rand seed 1)",
+            "config": {"workload": workload, "scene": args.scene, "grid": args.grid, "width": W,
+                       "height": H, "spp": args.spp, "depth": args.depth, "bvh": args.bvh,
+                       "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather to rank 0"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic(workload),
+                         "kernel_ms": round(avg_kernel_s * 1e3, 3),
+                         "algorithmic_bytes_per_launch": int(algo_bytes),
+                         "per_segment": {"box_tests": round(cst.box_tests / cst.segments, 3),
+                                         "prim_tests": round(cst.prim_tests / cst.segments, 3),
+                                         "hit_frac": round(cst.hits / cst.segments, 4)}},
+            "msamples_per_s": round(samples / wall / 1e6, 3),
+            "rays_per_sample": round(total_segs / samples, 4),
+            "scene_build_ms": round(t_scene * 1e3, 1),
+            "bvh": {"nodes": info.num_nodes, "depth": info.bvh_depth, "build_ms": round(info.build_ms, 1),
+                    "upload_ms": round(info.upload_ms, 1)},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args, s.desc, cam)
+            cb = line["cpu_baseline"]["value"]
+            line["speedup_vs_cpu"] = round(line["value"] / cb, 1) if cb else None
+        print(json.dumps(line), flush=True)
+    ds.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

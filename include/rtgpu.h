@@ -1,0 +1,232 @@
+/*
+ * rtgpu.h — C-ABI of the MI355X path-tracing library (librtgpu.so).
+ *
+ * This is the device boundary for the reference's per-pixel sample loop
+ *   camera::render -> ray_color -> bvh_node::hit / sphere::hit -> material::scatter
+ * (reference: src/core/camera.hpp:29-72, 180-232; src/accelerator/bvh_node.hpp:80-94;
+ *  src/hittable/sphere.hpp:47-93; src/core/material.hpp:51-206).
+ *
+ * The reference has no FFI: its "operator API" is the C++ virtual surface
+ * (hittable::hit, material::scatter, texture::value, camera::render). The C++ mirror of that
+ * surface (raytracing-practice_amd/include/) flattens a world into an rtg_scene_desc and
+ * calls the entry points below. Every signature uses plain pointers and sizes; nothing
+ * throws across the boundary; every call returns an rtg_status (0 = OK, negative = error)
+ * and rtg_last_error() describes the last failure on the calling thread.
+ *
+ * Threading: calls are blocking unless RTG_RENDER_ASYNC is set; one host thread (or process)
+ * per GPU; a scene handle is bound to the device it was created on and must not be used
+ * from two threads at once. The render RNG is stateless (counter-based), so calls are
+ * reentrant and results do not depend on tiling or scheduling.
+ */
+#ifndef RTGPU_H
+#define RTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTG_ABI_VERSION 1
+
+typedef int32_t rtg_status;
+#define RTG_OK 0
+#define RTG_E_INVALID (-1)     /* bad argument / malformed scene */
+#define RTG_E_HIP (-2)         /* HIP runtime error (message in rtg_last_error) */
+#define RTG_E_NODEVICE (-3)    /* no usable gfx950 device */
+#define RTG_E_NOMEM (-4)       /* host or device allocation failed */
+#define RTG_E_UNSUPPORTED (-5) /* feature not supported (e.g. BVH deeper than the kernel stack) */
+
+/* ---- primitives: replaces sphere (sphere.hpp:16-23, 32-44) and quad (quad.hpp:12-27) ---- */
+#define RTG_PRIM_SPHERE 1
+#define RTG_PRIM_QUAD 2
+
+typedef struct rtg_primitive {
+  int32_t kind;     /* RTG_PRIM_SPHERE | RTG_PRIM_QUAD */
+  int32_t material; /* index into rtg_scene_desc.materials */
+  double p0[3];     /* sphere: centre at time 0 (ray center.orig) | quad: Q */
+  double p1[3];     /* sphere: centre at time 1 (static: == p0)   | quad: u */
+  double p2[3];     /* sphere: unused                             | quad: v */
+  double radius;    /* sphere radius (sign kept, as the reference allows) */
+} rtg_primitive;
+
+/* ---- materials: replaces material.hpp:42-75, 80-111, 122-207, 223-240 ---- */
+#define RTG_MAT_LAMBERTIAN 1
+#define RTG_MAT_METAL 2
+#define RTG_MAT_DIELECTRIC 3
+#define RTG_MAT_DIFFUSE_LIGHT 4
+
+typedef struct rtg_material {
+  int32_t type;            /* RTG_MAT_* */
+  int32_t texture;         /* lambertian / diffuse_light: index into textures */
+  double albedo[3];        /* metal albedo */
+  double fuzz;             /* metal fuzz, already clamped to <= 1 (material.hpp:83) */
+  double refraction_index; /* dielectric */
+} rtg_material;
+
+/* ---- textures: replaces texture.hpp:25-41, 47-85, 91-122, 127-156 ---- */
+#define RTG_TEX_SOLID 1
+#define RTG_TEX_CHECKER 2
+#define RTG_TEX_IMAGE 3
+#define RTG_TEX_NOISE 4
+
+typedef struct rtg_texture {
+  int32_t type;    /* RTG_TEX_* */
+  int32_t even;    /* checker: texture index of even cells */
+  int32_t odd;     /* checker: texture index of odd cells */
+  int32_t image;   /* image: index into images */
+  int32_t perlin;  /* noise: index into perlins */
+  int32_t pad_;
+  double scale;    /* checker: constructor scale (inv_scale = 1.0f/scale, texture.hpp:50-51); noise: scale */
+  double color[3]; /* solid albedo */
+} rtg_texture;
+
+/* RGB8 image after rtw_image::convert_to_bytes (rtw_stb_image.hpp:137-169); rgb == NULL or
+ * height <= 0 means "could not load" and the texture returns cyan (texture.hpp:100-103). */
+typedef struct rtg_image {
+  int32_t width;
+  int32_t height;
+  const uint8_t* rgb; /* width*height*3 bytes, row 0 = top */
+} rtg_image;
+
+/* Perlin tables as drawn by perlin::perlin() (perlin.hpp:12-31). */
+typedef struct rtg_perlin {
+  double randvec[256][3];
+  int32_t perm_x[256];
+  int32_t perm_y[256];
+  int32_t perm_z[256];
+} rtg_perlin;
+
+/* BVH construction modes (the library always builds its own device BVH). */
+#define RTG_BVH_MEDIAN 0 /* bvh_node.hpp:25-77: longest axis, std::sort by bbox.min, median */
+#define RTG_BVH_SAH 1    /* binned SAH, leaves of <= 4 primitives */
+
+typedef struct rtg_scene_desc {
+  uint32_t abi_version; /* RTG_ABI_VERSION */
+  int32_t bvh_mode;     /* RTG_BVH_* */
+  const rtg_primitive* prims;
+  int64_t num_prims; /* object order == hittable_list order (tie-breaking, H9) */
+  const rtg_material* materials;
+  int32_t num_materials;
+  int32_t num_textures;
+  const rtg_texture* textures;
+  const rtg_image* images;
+  int32_t num_images;
+  int32_t num_perlins;
+  const rtg_perlin* perlins;
+} rtg_scene_desc;
+
+/* ---- camera: the reference's public fields (camera.hpp:13-25) ---- */
+typedef struct rtg_camera_desc {
+  double aspect_ratio;
+  int32_t image_width;
+  int32_t samples_per_pixel;
+  int32_t max_depth;
+  int32_t pad_;
+  double background[3];
+  double vfov;
+  double lookfrom[3];
+  double lookat[3];
+  double vup[3];
+  double defocus_angle;
+  double focus_dist;
+} rtg_camera_desc;
+
+/* camera::initialize() results (camera.hpp:76-136), computed in fp64 exactly as the reference. */
+typedef struct rtg_camera_params {
+  int32_t image_width;
+  int32_t image_height;
+  double pixel_samples_scale; /* float(1.0f / spp) (H7) */
+  double center[3];
+  double pixel00_loc[3];
+  double pixel_delta_u[3];
+  double pixel_delta_v[3];
+  double u[3], v[3], w[3];
+  double defocus_disk_u[3];
+  double defocus_disk_v[3];
+} rtg_camera_params;
+
+/* ---- one render call ---- */
+#define RTG_RENDER_OUT_DEVICE 0x1 /* out_rgb is a device pointer on the scene's device */
+#define RTG_RENDER_ASYNC 0x2      /* do not synchronize (requires OUT_DEVICE); stats filled later */
+#define RTG_RENDER_COUNT 0x4      /* also count box / primitive tests (slower, diagnostic) */
+
+typedef struct rtg_render_desc {
+  uint64_t seed;      /* run seed of the counter RNG */
+  int32_t row_begin;  /* first image row of this shard */
+  int32_t row_stride; /* rows row_begin + k*row_stride, k < row_count (interleaved tiling) */
+  int32_t row_count;  /* <= 0: every row reachable from row_begin with row_stride */
+  int32_t flags;      /* RTG_RENDER_* */
+  void* stream;       /* hipStream_t to launch on; NULL = the library's own stream */
+} rtg_render_desc;
+
+typedef struct rtg_render_stats {
+  uint64_t segments;   /* ray segments traced == world.hit() calls (camera.hpp:192) */
+  uint64_t samples;    /* camera samples == rows*width*spp */
+  uint64_t box_tests;  /* RTG_RENDER_COUNT only: child AABB tests */
+  uint64_t prim_tests; /* RTG_RENDER_COUNT only: sphere/quad tests */
+  uint64_t hits;       /* RTG_RENDER_COUNT only: segments that hit something */
+  double kernel_ms;    /* device time of the render kernel (HIP events on the launch stream) */
+} rtg_render_stats;
+
+typedef struct rtg_scene rtg_scene; /* opaque; owns the device copy of the scene */
+
+typedef struct rtg_scene_info {
+  int32_t device;
+  int32_t bvh_mode;
+  int64_t num_prims;
+  int64_t num_nodes;
+  int32_t bvh_depth;   /* longest root-to-leaf path in nodes */
+  int32_t stack_depth; /* traversal stack entries the selected kernel provides */
+  int64_t device_bytes;
+  double build_ms; /* host BVH build + flatten */
+  double upload_ms;
+} rtg_scene_info;
+
+/* Library identity. */
+uint32_t rtg_abi_version(void);
+const char* rtg_last_error(void);
+rtg_status rtg_device_count(int32_t* count);
+
+/* camera::initialize() on the host (camera.hpp:76-136). */
+rtg_status rtg_camera_resolve(const rtg_camera_desc* cam, rtg_camera_params* out);
+
+/* Scene lifetime. Host arrays are read during the call only; the scene owns device memory. */
+rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out);
+rtg_status rtg_scene_get_info(const rtg_scene* scene, rtg_scene_info* out);
+void rtg_scene_destroy(rtg_scene* scene);
+
+/* Render rows of the image. out_rgb receives row_count*image_width*3 floats: the linear,
+ * pre-gamma per-pixel mean  pixel_samples_scale * sum_s ray_color(...)  that the reference hands
+ * to write_color (camera.hpp:65), rows in shard order. */
+rtg_status rtg_render(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,
+                      float* out_rgb, rtg_render_stats* stats);
+
+/* Block until an RTG_RENDER_ASYNC render on `scene` finished; fills the deferred stats. */
+rtg_status rtg_render_wait(rtg_scene* scene, rtg_render_stats* stats);
+
+/* write_color (color.hpp:26-58) on the device: gamma 2, clamp [0, 0.999], int(256*x).
+ * in_rgb / out_rgb8 are device pointers on the scene's device; n_pixels pixels. */
+rtg_status rtg_resolve_rgb8(rtg_scene* scene, const float* in_rgb, uint8_t* out_rgb8,
+                            int64_t n_pixels, void* stream);
+
+/* Host-only: build the BVH the scene would use and report its topology (no GPU needed).
+ * nodes_out (optional, capacity max_nodes) receives per node: {left, right} child codes
+ * (>= 0 node index, < 0 leaf = -(1 + first_ref), leaf prim refs in refs_out) in DFS order
+ * plus the node's child boxes; returns counts in *num_nodes / *num_refs / *depth. */
+typedef struct rtg_bvh_node_host {
+  double lo[2][3]; /* child boxes (left, right) */
+  double hi[2][3];
+  int32_t child[2]; /* >= 0: node index; < 0: leaf -(1+first ref); INT32_MIN: empty */
+  int32_t count[2]; /* primitives in a leaf child */
+} rtg_bvh_node_host;
+
+rtg_status rtg_bvh_build_host(const rtg_scene_desc* desc, rtg_bvh_node_host* nodes_out,
+                              int64_t max_nodes, int64_t* refs_out, int64_t max_refs,
+                              int64_t* num_nodes, int64_t* num_refs, int32_t* depth);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTGPU_H */

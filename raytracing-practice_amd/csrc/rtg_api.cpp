@@ -1,0 +1,689 @@
+// rtg_api.cpp — the extern "C" boundary of librtgpu.so (include/rtgpu.h).
+//
+// Host responsibilities: validate the flat scene, run camera::initialize in fp64
+// (camera.hpp:76-136), build + flatten the BVH (rtg_bvh.cpp), upload the scene once, and launch
+// the gfx950 render kernel (rtg_kernels.hip) on the caller's stream. No CPU fallback exists:
+// without a usable device every entry point that renders returns RTG_E_NODEVICE / RTG_E_HIP.
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+
+#include "rtg_internal.hpp"
+
+namespace rtg {
+int kernel_stack_depth(int bvh_depth);
+hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
+                         bool count, hipStream_t stream);
+hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
+}  // namespace rtg
+
+using namespace rtg;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+rtg_status fail(rtg_status code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+rtg_status hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? RTG_E_NOMEM : RTG_E_HIP,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define RTG_HIP(call, what)                   \
+  do {                                        \
+    hipError_t e_ = (call);                   \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+// ---- fp64 vector helpers with the reference's operator semantics (vec3.hpp:100-155) ----
+struct D3 {
+  double x, y, z;
+};
+D3 d3(const double v[3]) { return D3{v[0], v[1], v[2]}; }
+D3 operator+(D3 a, D3 b) { return D3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+D3 operator-(D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+D3 operator-(D3 a) { return D3{-a.x, -a.y, -a.z}; }
+D3 operator*(double t, D3 a) { return D3{t * a.x, t * a.y, t * a.z}; }
+D3 operator/(D3 a, double t) { return (1 / t) * a; }
+double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+D3 cross(D3 a, D3 b) {
+  return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+D3 unit_vector(D3 v) { return v / std::sqrt(dot(v, v)); }
+void put(double o[3], D3 v) {
+  o[0] = v.x;
+  o[1] = v.y;
+  o[2] = v.z;
+}
+
+float round_down(double x) {
+  float f = static_cast<float>(x);
+  if (static_cast<double>(f) > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+float round_up(double x) {
+  float f = static_cast<float>(x);
+  if (static_cast<double>(f) < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  return f;
+}
+float ibits_to_float(int32_t i) {
+  float f;
+  std::memcpy(&f, &i, 4);
+  return f;
+}
+
+uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xbf58476d1ce4e5b9ull;
+  z ^= z >> 27;
+  z *= 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return z;
+}
+
+bool texture_uses_uv(const rtg_scene_desc* d, int32_t tex, int depth) {
+  if (depth > 16 || tex < 0 || tex >= d->num_textures) return false;
+  const rtg_texture& t = d->textures[tex];
+  if (t.type == RTG_TEX_IMAGE) return true;
+  if (t.type == RTG_TEX_CHECKER)
+    return texture_uses_uv(d, t.even, depth + 1) || texture_uses_uv(d, t.odd, depth + 1);
+  return false;
+}
+
+bool validate_texture(const rtg_scene_desc* d, int32_t tex, int depth, std::string* err) {
+  if (tex < 0 || tex >= d->num_textures) {
+    *err = "texture index out of range";
+    return false;
+  }
+  if (depth >= 16) {
+    *err = "checker textures nested deeper than 16 (or cyclic)";
+    return false;
+  }
+  const rtg_texture& t = d->textures[tex];
+  switch (t.type) {
+    case RTG_TEX_SOLID:
+      return true;
+    case RTG_TEX_CHECKER:
+      return validate_texture(d, t.even, depth + 1, err) && validate_texture(d, t.odd, depth + 1, err);
+    case RTG_TEX_IMAGE:
+      if (t.image >= d->num_images) {
+        *err = "image index out of range";
+        return false;
+      }
+      return true;
+    case RTG_TEX_NOISE:
+      if (t.perlin < 0 || t.perlin >= d->num_perlins) {
+        *err = "perlin index out of range";
+        return false;
+      }
+      return true;
+    default:
+      *err = "unknown texture type";
+      return false;
+  }
+}
+
+}  // namespace
+
+namespace rtg {
+
+void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
+  // camera::initialize (camera.hpp:76-136), fp64 with the reference's float-literal quirks.
+  const double pi = 3.1415926535897932385;
+  const int W = cam->image_width;
+  int H = static_cast<int>(W / cam->aspect_ratio);
+  H = (H < 1) ? 1 : H;
+  o->image_width = W;
+  o->image_height = H;
+  o->pixel_samples_scale = static_cast<double>(1.0f / cam->samples_per_pixel);
+  const double theta = cam->vfov * pi / 180.0f;
+  const double h = std::tan(theta / 2);
+  const double viewport_height = 2 * h * cam->focus_dist;
+  const double viewport_width = viewport_height * (static_cast<double>(W) / H);
+  const D3 center = d3(cam->lookfrom);
+  const D3 w = unit_vector(d3(cam->lookfrom) - d3(cam->lookat));
+  const D3 u = unit_vector(cross(d3(cam->vup), w));
+  const D3 v = cross(w, u);
+  const D3 viewport_u = viewport_width * u;
+  const D3 viewport_v = viewport_height * -v;
+  const D3 du = viewport_u / W;
+  const D3 dv = viewport_v / H;
+  const D3 upper_left = center - (cam->focus_dist * w) - viewport_u / 2 - viewport_v / 2;
+  const D3 p00 = upper_left + 0.5 * (du + dv);
+  const double defocus_radius = cam->focus_dist * std::tan(cam->defocus_angle * pi / 180.0f / 2.0f);
+  put(o->center, center);
+  put(o->pixel00_loc, p00);
+  put(o->pixel_delta_u, du);
+  put(o->pixel_delta_v, dv);
+  put(o->u, u);
+  put(o->v, v);
+  put(o->w, w);
+  put(o->defocus_disk_u, defocus_radius * u);
+  put(o->defocus_disk_v, defocus_radius * v);
+}
+
+bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
+  if (d->num_prims < 0 || (d->num_prims > 0 && !d->prims) || d->num_materials < 0 ||
+      (d->num_materials > 0 && !d->materials) || d->num_textures < 0 ||
+      (d->num_textures > 0 && !d->textures) || d->num_images < 0 ||
+      (d->num_images > 0 && !d->images) || d->num_perlins < 0 ||
+      (d->num_perlins > 0 && !d->perlins)) {
+    *err = "malformed scene descriptor (negative count or null array)";
+    return false;
+  }
+  for (int32_t m = 0; m < d->num_materials; ++m) {
+    const rtg_material& mt = d->materials[m];
+    if (mt.type == RTG_MAT_LAMBERTIAN || mt.type == RTG_MAT_DIFFUSE_LIGHT) {
+      if (!validate_texture(d, mt.texture, 0, err)) return false;
+    } else if (mt.type != RTG_MAT_METAL && mt.type != RTG_MAT_DIELECTRIC) {
+      *err = "unknown material type";
+      return false;
+    }
+  }
+  for (int64_t i = 0; i < d->num_prims; ++i) {
+    const rtg_primitive& p = d->prims[i];
+    if (p.kind != RTG_PRIM_SPHERE && p.kind != RTG_PRIM_QUAD) {
+      *err = "unknown primitive kind at index " + std::to_string(i);
+      return false;
+    }
+    if (p.material < 0 || p.material >= d->num_materials) {
+      *err = "primitive material index out of range at index " + std::to_string(i);
+      return false;
+    }
+  }
+
+  Bvh bvh;
+  if (!build_bvh(d, &bvh, err)) return false;
+  out->num_prims = d->num_prims;
+  out->num_nodes = static_cast<int64_t>(bvh.nodes.size());
+  out->depth = bvh.depth;
+
+  // primitives, laid out in first-reference order for locality
+  std::vector<int32_t> slot(d->num_prims, -1);
+  int32_t nsph = 0, nquad = 0;
+  out->refs.resize(bvh.refs.size());
+  for (size_t r = 0; r < bvh.refs.size(); ++r) {
+    const int64_t pid = bvh.refs[r];
+    const rtg_primitive& p = d->prims[pid];
+    if (slot[pid] < 0) {
+      if (p.kind == RTG_PRIM_SPHERE) {
+        slot[pid] = nsph++;
+        const float rec[8] = {static_cast<float>(p.p0[0]),
+                              static_cast<float>(p.p0[1]),
+                              static_cast<float>(p.p0[2]),
+                              static_cast<float>(p.radius),
+                              static_cast<float>(p.p1[0] - p.p0[0]),
+                              static_cast<float>(p.p1[1] - p.p0[1]),
+                              static_cast<float>(p.p1[2] - p.p0[2]),
+                              ibits_to_float(p.material)};
+        out->spheres.insert(out->spheres.end(), rec, rec + 8);
+      } else {
+        slot[pid] = nquad++;
+        // quad ctor (quad.hpp:12-27) in fp64, then rounded
+        const D3 Q = d3(p.p0), u = d3(p.p1), v = d3(p.p2);
+        const D3 n = cross(u, v);
+        const D3 normal = unit_vector(n);
+        const double D = dot(normal, Q);
+        const D3 w = n / dot(n, n);
+        const float rec[20] = {static_cast<float>(Q.x),      static_cast<float>(Q.y),
+                               static_cast<float>(Q.z),      static_cast<float>(D),
+                               static_cast<float>(u.x),      static_cast<float>(u.y),
+                               static_cast<float>(u.z),      ibits_to_float(p.material),
+                               static_cast<float>(v.x),      static_cast<float>(v.y),
+                               static_cast<float>(v.z),      0.0f,
+                               static_cast<float>(w.x),      static_cast<float>(w.y),
+                               static_cast<float>(w.z),      0.0f,
+                               static_cast<float>(normal.x), static_cast<float>(normal.y),
+                               static_cast<float>(normal.z), 0.0f};
+        out->quads.insert(out->quads.end(), rec, rec + 20);
+      }
+    }
+    out->refs[r] = (p.kind == RTG_PRIM_QUAD) ? (slot[pid] | kQuadRefBit) : slot[pid];
+  }
+
+  // child-pair nodes: 64 B, boxes rounded outward, leaf = ~((first << 3) | (count - 1))
+  out->nodes.resize(bvh.nodes.size() * 16);
+  for (size_t k = 0; k < bvh.nodes.size(); ++k) {
+    const BuildNode& n = bvh.nodes[k];
+    float lo[2][3], hi[2][3];
+    int32_t code[2];
+    for (int s = 0; s < 2; ++s) {
+      if (n.child[s] == kEmptyChild) {
+        for (int a = 0; a < 3; ++a) {
+          lo[s][a] = std::numeric_limits<float>::infinity();
+          hi[s][a] = -std::numeric_limits<float>::infinity();
+        }
+        code[s] = kEmptyChild;
+        continue;
+      }
+      for (int a = 0; a < 3; ++a) {
+        lo[s][a] = round_down(n.lo[s][a]);
+        hi[s][a] = round_up(n.hi[s][a]);
+      }
+      if (n.child[s] >= 0) {
+        code[s] = n.child[s];
+      } else {
+        const int64_t first = -(static_cast<int64_t>(n.child[s]) + 1);
+        const int32_t count = n.count[s];
+        if (count < 1 || count > 8 || first >= (int64_t(1) << 28)) {
+          *err = "BVH leaf not encodable";
+          return false;
+        }
+        code[s] = ~static_cast<int32_t>((first << 3) | (count - 1));
+      }
+    }
+    float* f = &out->nodes[k * 16];
+    f[0] = lo[0][0];
+    f[1] = lo[0][1];
+    f[2] = lo[0][2];
+    f[3] = hi[0][0];
+    f[4] = hi[0][1];
+    f[5] = hi[0][2];
+    f[6] = lo[1][0];
+    f[7] = lo[1][1];
+    f[8] = lo[1][2];
+    f[9] = hi[1][0];
+    f[10] = hi[1][1];
+    f[11] = hi[1][2];
+    f[12] = ibits_to_float(code[0]);
+    f[13] = ibits_to_float(code[1]);
+    f[14] = 0.0f;
+    f[15] = 0.0f;
+  }
+
+  // materials {type, texture, fuzz, eta}, {albedo.xyz, uses_uv}
+  for (int32_t m = 0; m < d->num_materials; ++m) {
+    const rtg_material& mt = d->materials[m];
+    const double fuzz = mt.fuzz < 1.0f ? mt.fuzz : 1.0f;  // metal ctor clamp (material.hpp:83)
+    const bool uv = (mt.type == RTG_MAT_LAMBERTIAN || mt.type == RTG_MAT_DIFFUSE_LIGHT) &&
+                    texture_uses_uv(d, mt.texture, 0);
+    const float rec[8] = {ibits_to_float(mt.type),
+                          ibits_to_float(mt.texture),
+                          static_cast<float>(fuzz),
+                          static_cast<float>(mt.refraction_index),
+                          static_cast<float>(mt.albedo[0]),
+                          static_cast<float>(mt.albedo[1]),
+                          static_cast<float>(mt.albedo[2]),
+                          ibits_to_float(uv ? 1 : 0)};
+    out->materials.insert(out->materials.end(), rec, rec + 8);
+  }
+  // textures {type, even, odd, scale'}, {color.xyz, image|perlin}
+  uint64_t texel_off = 0;
+  for (int32_t im = 0; im < d->num_images; ++im) {
+    const rtg_image& img = d->images[im];
+    const bool ok = img.rgb != nullptr && img.width > 0 && img.height > 0;
+    const int32_t hdr[4] = {ok ? img.width : 0, ok ? img.height : 0,
+                            static_cast<int32_t>(texel_off & 0xffffffffu),
+                            static_cast<int32_t>(texel_off >> 32)};
+    out->image_hdr.insert(out->image_hdr.end(), hdr, hdr + 4);
+    if (ok) {
+      const uint64_t bytes = static_cast<uint64_t>(img.width) * img.height * 3;
+      out->texels.insert(out->texels.end(), img.rgb, img.rgb + bytes);
+      texel_off += bytes;
+      while (texel_off % 16) {
+        out->texels.push_back(0);
+        ++texel_off;
+      }
+    }
+  }
+  for (int32_t t = 0; t < d->num_textures; ++t) {
+    const rtg_texture& tx = d->textures[t];
+    float scale = 0.0f;
+    int32_t aux = -1;
+    if (tx.type == RTG_TEX_CHECKER) scale = static_cast<float>(1.0f / tx.scale);  // texture.hpp:50-51
+    if (tx.type == RTG_TEX_NOISE) {
+      scale = static_cast<float>(tx.scale);
+      aux = tx.perlin;
+    }
+    if (tx.type == RTG_TEX_IMAGE) aux = (tx.image >= 0 && tx.image < d->num_images) ? tx.image : -1;
+    const float rec[8] = {ibits_to_float(tx.type),
+                          ibits_to_float(tx.even),
+                          ibits_to_float(tx.odd),
+                          scale,
+                          static_cast<float>(tx.color[0]),
+                          static_cast<float>(tx.color[1]),
+                          static_cast<float>(tx.color[2]),
+                          ibits_to_float(aux)};
+    out->textures.insert(out->textures.end(), rec, rec + 8);
+  }
+  for (int32_t pt = 0; pt < d->num_perlins; ++pt) {
+    const rtg_perlin& pl = d->perlins[pt];
+    for (int i = 0; i < 256; ++i) {
+      const float v[4] = {static_cast<float>(pl.randvec[i][0]), static_cast<float>(pl.randvec[i][1]),
+                          static_cast<float>(pl.randvec[i][2]), 0.0f};
+      out->perlin_vec.insert(out->perlin_vec.end(), v, v + 4);
+    }
+    for (int i = 0; i < 256; ++i) {
+      if (pl.perm_x[i] < 0 || pl.perm_x[i] > 255 || pl.perm_y[i] < 0 || pl.perm_y[i] > 255 ||
+          pl.perm_z[i] < 0 || pl.perm_z[i] > 255) {
+        *err = "perlin permutation entry out of [0, 255]";
+        return false;
+      }
+    }
+    out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_x, pl.perm_x + 256);
+    out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_y, pl.perm_y + 256);
+    out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_z, pl.perm_z + 256);
+  }
+  return true;
+}
+
+}  // namespace rtg
+
+struct rtg_scene {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  void* dmem = nullptr;  // one allocation for all scene arrays
+  size_t dbytes = 0;
+  unsigned long long* counters = nullptr;  // device [8]
+  unsigned long long* host_counters = nullptr;  // pinned [8]
+  DevScene dev{};
+  rtg_scene_info info{};
+  // deferred (async) render state
+  bool pending = false;
+  hipStream_t pending_stream = nullptr;
+  uint64_t pending_samples = 0;
+};
+
+extern "C" {
+
+uint32_t rtg_abi_version(void) { return RTG_ABI_VERSION; }
+
+const char* rtg_last_error(void) { return g_last_error.c_str(); }
+
+rtg_status rtg_device_count(int32_t* count) {
+  if (!count) return fail(RTG_E_INVALID, "count is NULL");
+  int n = 0;
+  const hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(RTG_E_NODEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = n;
+  return RTG_OK;
+}
+
+rtg_status rtg_camera_resolve(const rtg_camera_desc* cam, rtg_camera_params* out) {
+  if (!cam || !out) return fail(RTG_E_INVALID, "null argument");
+  if (cam->image_width <= 0 || cam->samples_per_pixel <= 0)
+    return fail(RTG_E_INVALID, "image_width and samples_per_pixel must be positive");
+  resolve_camera(cam, out);
+  return RTG_OK;
+}
+
+rtg_status rtg_bvh_build_host(const rtg_scene_desc* desc, rtg_bvh_node_host* nodes_out,
+                              int64_t max_nodes, int64_t* refs_out, int64_t max_refs,
+                              int64_t* num_nodes, int64_t* num_refs, int32_t* depth) {
+  if (!desc) return fail(RTG_E_INVALID, "desc is NULL");
+  if (desc->num_prims < 0 || (desc->num_prims > 0 && !desc->prims))
+    return fail(RTG_E_INVALID, "malformed primitive array");
+  Bvh bvh;
+  std::string err;
+  if (!build_bvh(desc, &bvh, &err)) return fail(RTG_E_INVALID, err);
+  if (num_nodes) *num_nodes = static_cast<int64_t>(bvh.nodes.size());
+  if (num_refs) *num_refs = static_cast<int64_t>(bvh.refs.size());
+  if (depth) *depth = bvh.depth;
+  if (nodes_out) {
+    const int64_t n = std::min<int64_t>(max_nodes, bvh.nodes.size());
+    for (int64_t k = 0; k < n; ++k) {
+      const BuildNode& b = bvh.nodes[k];
+      rtg_bvh_node_host& h = nodes_out[k];
+      std::memcpy(h.lo, b.lo, sizeof(h.lo));
+      std::memcpy(h.hi, b.hi, sizeof(h.hi));
+      h.child[0] = b.child[0];
+      h.child[1] = b.child[1];
+      h.count[0] = b.count[0];
+      h.count[1] = b.count[1];
+    }
+  }
+  if (refs_out) {
+    const int64_t n = std::min<int64_t>(max_refs, bvh.refs.size());
+    for (int64_t k = 0; k < n; ++k) refs_out[k] = bvh.refs[k];
+  }
+  return RTG_OK;
+}
+
+rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out) {
+  if (!desc || !out) return fail(RTG_E_INVALID, "null argument");
+  *out = nullptr;
+  if (desc->abi_version != RTG_ABI_VERSION)
+    return fail(RTG_E_INVALID, "abi_version mismatch (expected " +
+                                   std::to_string(RTG_ABI_VERSION) + ")");
+  // validate + compile first (host only), so malformed scenes report RTG_E_INVALID anywhere
+  const auto t0 = std::chrono::steady_clock::now();
+  HostScene hs;
+  std::string err;
+  if (!compile_scene(desc, &hs, &err)) return fail(RTG_E_INVALID, err);
+  const int stack = kernel_stack_depth(hs.depth);
+  if (stack < 0)
+    return fail(RTG_E_UNSUPPORTED, "BVH depth " + std::to_string(hs.depth) +
+                                       " exceeds the deepest kernel stack (64)");
+  const auto t1 = std::chrono::steady_clock::now();
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(RTG_E_NODEVICE, "no HIP device available (librtgpu has no CPU fallback)");
+  if (device < 0 || device >= ndev) return fail(RTG_E_INVALID, "device index out of range");
+  RTG_HIP(hipSetDevice(device), "hipSetDevice");
+  hipDeviceProp_t prop;
+  RTG_HIP(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(RTG_E_NODEVICE, std::string("device is ") + prop.gcnArchName +
+                                    ", this build targets gfx950 only");
+
+  // one device allocation, 256-B aligned sub-buffers
+  struct Part {
+    const void* src;
+    size_t bytes;
+    size_t off;
+  };
+  Part parts[9] = {
+      {hs.nodes.data(), hs.nodes.size() * 4, 0},       {hs.refs.data(), hs.refs.size() * 4, 0},
+      {hs.spheres.data(), hs.spheres.size() * 4, 0},   {hs.quads.data(), hs.quads.size() * 4, 0},
+      {hs.materials.data(), hs.materials.size() * 4, 0}, {hs.textures.data(), hs.textures.size() * 4, 0},
+      {hs.image_hdr.data(), hs.image_hdr.size() * 4, 0}, {hs.texels.data(), hs.texels.size(), 0},
+      {hs.perlin_vec.data(), hs.perlin_vec.size() * 4, 0}};
+  size_t total = 0;
+  for (Part& p : parts) {
+    p.off = total;
+    total += (p.bytes + 255) & ~size_t(255);
+  }
+  const size_t perm_off = total;
+  total += (hs.perlin_perm.size() * 4 + 255) & ~size_t(255);
+  total = std::max<size_t>(total, 256);
+
+  rtg_scene* s = new (std::nothrow) rtg_scene();
+  if (!s) return fail(RTG_E_NOMEM, "host allocation failed");
+  s->device = device;
+  auto cleanup = [&](rtg_status st) {
+    rtg_scene_destroy(s);
+    return st;
+  };
+  hipError_t e = hipMalloc(&s->dmem, total);
+  if (e != hipSuccess) return cleanup(hip_fail(e, "hipMalloc(scene)"));
+  s->dbytes = total;
+  if ((e = hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking)) != hipSuccess)
+    return cleanup(hip_fail(e, "hipStreamCreate"));
+  if ((e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess)
+    return cleanup(hip_fail(e, "hipEventCreate"));
+  if ((e = hipMalloc(&s->counters, 8 * sizeof(unsigned long long))) != hipSuccess)
+    return cleanup(hip_fail(e, "hipMalloc(counters)"));
+  if ((e = hipHostMalloc(&s->host_counters, 8 * sizeof(unsigned long long))) != hipSuccess)
+    return cleanup(hip_fail(e, "hipHostMalloc(counters)"));
+  char* base = static_cast<char*>(s->dmem);
+  for (const Part& p : parts) {
+    if (p.bytes == 0) continue;
+    if ((e = hipMemcpyAsync(base + p.off, p.src, p.bytes, hipMemcpyHostToDevice, s->own_stream)) !=
+        hipSuccess)
+      return cleanup(hip_fail(e, "hipMemcpy(scene)"));
+  }
+  if (!hs.perlin_perm.empty() &&
+      (e = hipMemcpyAsync(base + perm_off, hs.perlin_perm.data(), hs.perlin_perm.size() * 4,
+                          hipMemcpyHostToDevice, s->own_stream)) != hipSuccess)
+    return cleanup(hip_fail(e, "hipMemcpy(perlin)"));
+  if ((e = hipStreamSynchronize(s->own_stream)) != hipSuccess)
+    return cleanup(hip_fail(e, "hipStreamSynchronize(upload)"));
+  const auto t2 = std::chrono::steady_clock::now();
+
+  s->dev.nodes = reinterpret_cast<const float4*>(base + parts[0].off);
+  s->dev.refs = reinterpret_cast<const int32_t*>(base + parts[1].off);
+  s->dev.spheres = reinterpret_cast<const float4*>(base + parts[2].off);
+  s->dev.quads = reinterpret_cast<const float4*>(base + parts[3].off);
+  s->dev.materials = reinterpret_cast<const float4*>(base + parts[4].off);
+  s->dev.textures = reinterpret_cast<const float4*>(base + parts[5].off);
+  s->dev.images = reinterpret_cast<const int4*>(base + parts[6].off);
+  s->dev.texels = reinterpret_cast<const uint8_t*>(base + parts[7].off);
+  s->dev.perlin_vec = reinterpret_cast<const float4*>(base + parts[8].off);
+  s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
+  s->dev.num_nodes = hs.num_nodes;
+
+  s->info.device = device;
+  s->info.bvh_mode = desc->bvh_mode;
+  s->info.num_prims = hs.num_prims;
+  s->info.num_nodes = hs.num_nodes;
+  s->info.bvh_depth = hs.depth;
+  s->info.stack_depth = stack;
+  s->info.device_bytes = static_cast<int64_t>(total);
+  s->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  s->info.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  *out = s;
+  return RTG_OK;
+}
+
+rtg_status rtg_scene_get_info(const rtg_scene* scene, rtg_scene_info* out) {
+  if (!scene || !out) return fail(RTG_E_INVALID, "null argument");
+  *out = scene->info;
+  return RTG_OK;
+}
+
+void rtg_scene_destroy(rtg_scene* s) {
+  if (!s) return;
+  // teardown: errors cannot be reported from a void destructor, they are deliberately dropped
+  (void)hipSetDevice(s->device);
+  if (s->pending && s->pending_stream) (void)hipStreamSynchronize(s->pending_stream);
+  if (s->dmem) (void)hipFree(s->dmem);
+  if (s->counters) (void)hipFree(s->counters);
+  if (s->host_counters) (void)hipHostFree(s->host_counters);
+  if (s->ev0) (void)hipEventDestroy(s->ev0);
+  if (s->ev1) (void)hipEventDestroy(s->ev1);
+  if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
+  delete s;
+}
+
+static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
+  RTG_HIP(hipEventSynchronize(s->ev1), "render kernel");
+  float ms = 0.0f;
+  RTG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1), "hipEventElapsedTime");
+  RTG_HIP(hipStreamSynchronize(s->pending_stream), "render stream");
+  const unsigned long long* c = s->host_counters;
+  s->pending = false;
+  if (c[4] != 0) return fail(RTG_E_UNSUPPORTED, "BVH traversal stack overflow");
+  if (stats) {
+    stats->segments = c[0];
+    stats->box_tests = c[1];
+    stats->prim_tests = c[2];
+    stats->hits = c[3];
+    stats->samples = s->pending_samples;
+    stats->kernel_ms = ms;
+  }
+  return RTG_OK;
+}
+
+rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,
+                      float* out_rgb, rtg_render_stats* stats) {
+  if (!s || !cam || !job || !out_rgb) return fail(RTG_E_INVALID, "null argument");
+  if (cam->image_width <= 0 || cam->samples_per_pixel <= 0)
+    return fail(RTG_E_INVALID, "image_width and samples_per_pixel must be positive");
+  if (job->row_stride <= 0 || job->row_begin < 0) return fail(RTG_E_INVALID, "bad row range");
+  const bool dev_out = (job->flags & RTG_RENDER_OUT_DEVICE) != 0;
+  const bool async = (job->flags & RTG_RENDER_ASYNC) != 0;
+  if (async && !dev_out) return fail(RTG_E_INVALID, "RTG_RENDER_ASYNC requires RTG_RENDER_OUT_DEVICE");
+  if (s->pending) return fail(RTG_E_INVALID, "a previous async render was not waited for");
+
+  rtg_camera_params cp;
+  resolve_camera(cam, &cp);
+  const int W = cp.image_width, H = cp.image_height;
+  if (job->row_begin >= H) return fail(RTG_E_INVALID, "row_begin beyond image height");
+  const int reachable = (H - 1 - job->row_begin) / job->row_stride + 1;
+  const int rows = job->row_count <= 0 ? reachable : job->row_count;
+  if (rows > reachable) return fail(RTG_E_INVALID, "row_count reaches past the image");
+  if (static_cast<int64_t>(W) * H >= (int64_t(1) << 32))
+    return fail(RTG_E_INVALID, "image larger than 2^32 pixels");
+
+  DevCamera dc{};
+  for (int k = 0; k < 3; ++k) {
+    dc.center[k] = static_cast<float>(cp.center[k]);
+    dc.pixel00[k] = static_cast<float>(cp.pixel00_loc[k]);
+    dc.du[k] = static_cast<float>(cp.pixel_delta_u[k]);
+    dc.dv[k] = static_cast<float>(cp.pixel_delta_v[k]);
+    dc.defu[k] = static_cast<float>(cp.defocus_disk_u[k]);
+    dc.defv[k] = static_cast<float>(cp.defocus_disk_v[k]);
+    dc.background[k] = static_cast<float>(cam->background[k]);
+  }
+  dc.scale = static_cast<float>(cp.pixel_samples_scale);
+  dc.width = W;
+  dc.height = H;
+  dc.spp = cam->samples_per_pixel;
+  dc.max_depth = cam->max_depth;
+  dc.defocus = cam->defocus_angle <= 0.0f ? 0 : 1;  // camera.hpp:155
+
+  RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+  hipStream_t stream = job->stream ? static_cast<hipStream_t>(job->stream) : s->own_stream;
+  const size_t out_bytes = static_cast<size_t>(rows) * W * 3 * sizeof(float);
+  float* dout = out_rgb;
+  if (!dev_out) {
+    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dout), out_bytes, stream), "hipMallocAsync(out)");
+  }
+  DevJob dj{};
+  dj.seed_mix = mix64(job->seed);
+  dj.row_begin = job->row_begin;
+  dj.row_stride = job->row_stride;
+  dj.row_count = rows;
+  dj.out = dout;
+  dj.counters = s->counters;
+  RTG_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
+  RTG_HIP(launch_render(s->dev, dc, dj, s->info.stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
+                        stream),
+          "render kernel launch");
+  RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
+  RTG_HIP(hipMemcpyAsync(s->host_counters, s->counters, 8 * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, stream),
+          "hipMemcpyAsync(counters)");
+  if (!dev_out) {
+    RTG_HIP(hipMemcpyAsync(out_rgb, dout, out_bytes, hipMemcpyDeviceToHost, stream), "hipMemcpy(out)");
+    RTG_HIP(hipFreeAsync(dout, stream), "hipFreeAsync(out)");
+  }
+  s->pending = true;
+  s->pending_stream = stream;
+  s->pending_samples = static_cast<uint64_t>(rows) * W * cam->samples_per_pixel;
+  if (async) return RTG_OK;
+  return collect_stats(s, stats);
+}
+
+rtg_status rtg_render_wait(rtg_scene* s, rtg_render_stats* stats) {
+  if (!s) return fail(RTG_E_INVALID, "null scene");
+  if (!s->pending) return fail(RTG_E_INVALID, "no render pending");
+  RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+  return collect_stats(s, stats);
+}
+
+rtg_status rtg_resolve_rgb8(rtg_scene* s, const float* in_rgb, uint8_t* out_rgb8, int64_t n_pixels,
+                            void* stream) {
+  if (!s || !in_rgb || !out_rgb8) return fail(RTG_E_INVALID, "null argument");
+  RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+  hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->own_stream;
+  RTG_HIP(launch_resolve(in_rgb, out_rgb8, n_pixels, st), "resolve kernel launch");
+  if (!stream) RTG_HIP(hipStreamSynchronize(st), "resolve kernel");
+  return RTG_OK;
+}
+
+}  // extern "C"

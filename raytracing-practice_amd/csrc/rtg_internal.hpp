@@ -1,0 +1,107 @@
+// rtg_internal.hpp — layouts shared by the host scene compiler (rtg_api.cpp, rtg_bvh.cpp) and the
+// gfx950 kernels (rtg_kernels.hip). Not part of the public C-ABI (include/rtgpu.h).
+//
+// Device scene layout in HBM (all 16-B aligned, read-only during a render):
+//   nodes    : float4[4*num_nodes]   64-B child-pair BVH node (both child boxes + child codes)
+//   refs     : int32[num_refs]       leaf primitive references (bit 30 = quad)
+//   spheres  : float4[2*num_spheres] {c0.xyz, r}, {dc.xyz, material}
+//   quads    : float4[5*num_quads]   {Q.xyz, D}, {u.xyz, material}, {v.xyz, -}, {w.xyz, -}, {n.xyz, -}
+//   materials: float4[2*num_mats]    {type, texture, fuzz, eta}, {albedo.xyz, -}
+//   textures : float4[2*num_tex]     {type, even, odd, scale}, {color.xyz, image|perlin}
+//   images   : int4[num_images]      {width, height, byte offset lo, byte offset hi} + uint8 texels
+//   perlin   : per table float4 randvec[256] then int32 perm[3][256]
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rtgpu.h"
+
+namespace rtg {
+
+constexpr int32_t kEmptyChild = INT32_MIN;  // child slot with an inverted box; never visited
+constexpr int32_t kQuadRefBit = 1 << 30;
+
+// A float view of the scene, ready for upload. Produced on the host from rtg_scene_desc.
+struct HostScene {
+  std::vector<float> nodes;      // 16 floats per node
+  std::vector<int32_t> refs;
+  std::vector<float> spheres;    // 8 floats per sphere
+  std::vector<float> quads;      // 20 floats per quad
+  std::vector<float> materials;  // 8 floats per material
+  std::vector<float> textures;   // 8 floats per texture
+  std::vector<int32_t> image_hdr;  // 4 ints per image
+  std::vector<uint8_t> texels;
+  std::vector<float> perlin_vec;   // 4 floats * 256 per table
+  std::vector<int32_t> perlin_perm;  // 3*256 per table
+  int64_t num_nodes = 0;
+  int32_t depth = 0;
+  int64_t num_prims = 0;
+};
+
+// Double-precision BVH produced by the builders (child-pair form, pre-order DFS).
+struct BuildNode {
+  double lo[2][3];
+  double hi[2][3];
+  int32_t child[2];
+  int32_t count[2];
+};
+
+struct Bvh {
+  std::vector<BuildNode> nodes;
+  std::vector<int64_t> refs;  // primitive indices (into desc->prims)
+  int32_t depth = 0;
+};
+
+// aabb of one primitive exactly as the reference computes it (aabb.hpp:30-48,135-154;
+// sphere.hpp:16-44; quad.hpp:30-38).
+void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]);
+
+bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err);
+bool compile_scene(const rtg_scene_desc* desc, HostScene* out, std::string* err);
+void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* out);
+
+// Kernel-side camera / job parameters (passed by value to the kernels).
+struct DevCamera {
+  float center[3];
+  float pixel00[3];
+  float du[3];
+  float dv[3];
+  float defu[3];
+  float defv[3];
+  float background[3];
+  float scale;  // pixel_samples_scale
+  int32_t width;
+  int32_t height;
+  int32_t spp;
+  int32_t max_depth;
+  int32_t defocus;  // defocus_angle > 0
+};
+
+struct DevScene {
+  const float4* nodes;
+  const int32_t* refs;
+  const float4* spheres;
+  const float4* quads;
+  const float4* materials;
+  const float4* textures;
+  const int4* images;
+  const uint8_t* texels;
+  const float4* perlin_vec;
+  const int32_t* perlin_perm;
+  int64_t num_nodes;
+};
+
+struct DevJob {
+  uint64_t seed_mix;
+  int32_t row_begin;
+  int32_t row_stride;
+  int32_t row_count;
+  int32_t pad_;
+  float* out;
+  unsigned long long* counters;  // [0] segments, [1] box tests, [2] prim tests, [3] hits
+};
+
+}  // namespace rtg

@@ -1,0 +1,571 @@
+// rtg_kernels.hip — gfx950 kernels of the per-pixel sample loop.
+//
+// Replaces (reference file:line):
+//   camera::render 29-72, get_ray 139-177, ray_color 180-232      (src/core/camera.hpp)
+//   hittable_list::hit 40-64 + bvh_node::hit 80-94 + aabb::hit 61-112
+//   sphere::hit 47-93 / get_sphere_uv 100-111, quad::hit 44-114
+//   material::scatter / emitted (src/core/material.hpp:51-240)
+//   texture::value (src/core/texture.hpp:34-151), perlin::turb (src/core/perlin.hpp:95-158,219-255)
+//   write_color (src/common/color.hpp:14-58)
+//
+// Execution model: one lane owns one pixel of the shard and walks its samples in order
+// s = 0..spp-1, so the per-pixel sum is accumulated in exactly the order the reference uses
+// (camera.hpp:55-62). Paths are regenerated in place: when a lane's path ends it immediately
+// starts its next sample, so every lane of a wave traces one segment per loop trip until the
+// lane has finished all of its samples (no per-bounce wave drain). A 64-lane wave covers an
+// 8x8 pixel tile; a 256-thread workgroup covers 16x16. Each lane's BVH stack lives in LDS
+// laid out [depth][lane] (bank-conflict-free for ds_read_b32/ds_write_b32).
+//
+// Numerics: the fp32 spec in DESIGN.md ("rtg-f32"); compiled with -ffp-contract=off so every
+// expression rounds as written and matches the CPU restatement in oracle/cpu_ref.c. The only
+// fused ops are the slab tests, which only cull (boxes are rounded outward on the host).
+#include <cstdint>
+
+#include "rtg_internal.hpp"
+
+namespace rtg {
+namespace {
+
+constexpr float kTMin = 0.001f;  // interval(0.001, infinity), camera.hpp:192
+constexpr float kPi = 3.14159265358979323846f;
+constexpr int kMaxRejectTries = 64;
+constexpr int kMaxTexNesting = 16;
+
+struct V3 {
+  float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 scl(float t, V3 a) { return v3(t * a.x, t * a.y, t * a.z); }
+__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ V3 unit(V3 a) {  // unit_vector: v / v.length() == (1/len) * v
+  const float len = sqrtf(dot(a, a));
+  return scl(1.0f / len, a);
+}
+__device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
+__device__ __forceinline__ int ibits(float f) { return __float_as_int(f); }
+
+// ---------------------------------------------------------------------------------------
+// Counter RNG: PCG32 (XSH-RR) seeded per (pixel, sample) by a splitmix64
+// finaliser. Replaces the global glibc rand() stream (rtweekend.hpp:23-39, hazard H1).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xbf58476d1ce4e5b9ull;
+  z ^= z >> 27;
+  z *= 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return z;
+}
+__device__ __forceinline__ uint32_t pcg_next(uint64_t& s) {
+  const uint64_t old = s;
+  s = old * 6364136223846793005ull + 1442695040888963407ull;
+  const uint32_t xs = static_cast<uint32_t>(((old >> 18) ^ old) >> 27);
+  const uint32_t rot = static_cast<uint32_t>(old >> 59);
+  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+__device__ __forceinline__ float uniform(uint64_t& s) {  // random_double(), [0,1), 24 bits
+  return static_cast<float>(pcg_next(s) >> 8) * 5.9604644775390625e-8f;
+}
+__device__ __forceinline__ float uniform_m11(uint64_t& s) {  // random_double(-1, 1)
+  return -1.0f + 2.0f * uniform(s);
+}
+
+// random_unit_vector (vec3.hpp:172-184), draws x, y, z in that order.
+__device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
+  for (int k = 0; k < kMaxRejectTries; ++k) {
+    const float x = uniform_m11(s);
+    const float y = uniform_m11(s);
+    const float z = uniform_m11(s);
+    const float lensq = x * x + y * y + z * z;
+    if (0.0f < lensq && lensq <= 1.0f) return scl(1.0f / sqrtf(lensq), v3(x, y, z));
+  }
+  return v3(1.0f, 0.0f, 0.0f);
+}
+
+// ---------------------------------------------------------------------------------------
+// Geometry
+// sphere::hit (sphere.hpp:47-93) with the fp32-robust root form of DESIGN.md: c = |oc|^2 - r^2
+// is formed in f64, the near root as c/q. Returns the root or -1.
+__device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float time, float tmin,
+                                          float tmax) {
+  const V3 C = v3(s0.x + time * s1.x, s0.y + time * s1.y, s0.z + time * s1.z);
+  const V3 oc = sub(o, C);
+  const float a = dot(d, d);
+  const float hb = dot(oc, d);
+  const double ox = static_cast<double>(o.x) - static_cast<double>(C.x);
+  const double oy = static_cast<double>(o.y) - static_cast<double>(C.y);
+  const double oz = static_cast<double>(o.z) - static_cast<double>(C.z);
+  const double r = static_cast<double>(s0.w);
+  const float c = static_cast<float>((ox * ox + oy * oy + oz * oz) - r * r);
+  const float disc = hb * hb - a * c;
+  if (disc < 0.0f) return -1.0f;
+  const float sq = sqrtf(disc);
+  const float q = -(hb + copysignf(sq, hb));
+  if (q == 0.0f || a == 0.0f) return -1.0f;
+  const float t0 = q / a;
+  const float t1 = c / q;
+  const float lo = fminf(t0, t1);
+  const float hi = fmaxf(t0, t1);
+  if (tmin < lo && lo < tmax) return lo;
+  if (tmin < hi && hi < tmax) return hi;
+  return -1.0f;
+}
+
+// quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
+__device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin, float tmax) {
+  const float4 q0 = q[0], q4 = q[4];
+  const V3 n = xyz(q4);
+  const float denom = dot(n, d);
+  if (fabsf(denom) < 1e-8f) return -1.0f;
+  const double dn = static_cast<double>(n.x) * o.x + static_cast<double>(n.y) * o.y +
+                    static_cast<double>(n.z) * o.z;
+  const float num = static_cast<float>(static_cast<double>(q0.w) - dn);
+  const float t = num / denom;
+  if (!(tmin <= t && t <= tmax)) return -1.0f;
+  const V3 p = add(o, scl(t, d));
+  const V3 hp = sub(p, xyz(q0));
+  const V3 u = xyz(q[1]), v = xyz(q[2]), w = xyz(q[3]);
+  const float alpha = dot(w, cross(hp, v));
+  const float beta = dot(w, cross(u, hp));
+  if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return -1.0f;
+  return t;
+}
+
+template <bool COUNT>
+struct Counts {
+  uint32_t box = 0, prim = 0;
+};
+
+// Closest hit over the child-pair BVH (replaces hittable_list::hit -> bvh_node::hit ->
+// aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
+// traversal: the nearer child first, the farther pushed on the lane's LDS stack.
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, float time,
+                                               float& tbest, int32_t* stk, Counts<COUNT>& cnt,
+                                               bool& overflow) {
+  int32_t best = -1;
+  if (S.num_nodes == 0) return best;
+  const V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y),
+                    __builtin_amdgcn_rcpf(d.z));
+  const V3 oi = v3(-o.x * inv.x, -o.y * inv.y, -o.z * inv.z);
+  int sp = 0;
+  int32_t todo = 0;
+  while (true) {
+    if (todo >= 0) {
+      const float4* n = S.nodes + static_cast<int64_t>(todo) * 4;
+      const float4 a = n[0], b = n[1], c = n[2];
+      const int4 ch = *reinterpret_cast<const int4*>(n + 3);
+      if (COUNT) cnt.box += 2;
+      // left box lo=(a.x,a.y,a.z) hi=(a.w,b.x,b.y); right lo=(b.z,b.w,c.x) hi=(c.y,c.z,c.w)
+      const float l0x = fmaf(a.x, inv.x, oi.x), l1x = fmaf(a.w, inv.x, oi.x);
+      const float l0y = fmaf(a.y, inv.y, oi.y), l1y = fmaf(b.x, inv.y, oi.y);
+      const float l0z = fmaf(a.z, inv.z, oi.z), l1z = fmaf(b.y, inv.z, oi.z);
+      const float r0x = fmaf(b.z, inv.x, oi.x), r1x = fmaf(c.y, inv.x, oi.x);
+      const float r0y = fmaf(b.w, inv.y, oi.y), r1y = fmaf(c.z, inv.y, oi.y);
+      const float r0z = fmaf(c.x, inv.z, oi.z), r1z = fmaf(c.w, inv.z, oi.z);
+      const float ln = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), kTMin));
+      const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tbest));
+      const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kTMin));
+      const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tbest));
+      const bool hl = ln <= lf;
+      const bool hr = rn <= rf;
+      if (hl && hr) {
+        const bool lfirst = ln <= rn;
+        const int32_t nearc = lfirst ? ch.x : ch.y;
+        const int32_t farc = lfirst ? ch.y : ch.x;
+        if (sp < STACK) {
+          stk[sp * 64] = farc;
+          ++sp;
+        } else {
+          overflow = true;
+        }
+        todo = nearc;
+        continue;
+      }
+      if (hl || hr) {
+        todo = hl ? ch.x : ch.y;
+        continue;
+      }
+    } else {
+      const int32_t code = ~todo;
+      const int32_t first = code >> 3;
+      const int32_t count = (code & 7) + 1;
+      for (int k = 0; k < count; ++k) {
+        const int32_t ref = S.refs[first + k];
+        float t;
+        if (COUNT) cnt.prim += 1;
+        if (ref & kQuadRefBit) {
+          t = quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest);
+        } else {
+          const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
+          t = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, tbest);
+        }
+        if (t > 0.0f) {  // t > tmin >= 0.001 on a hit
+          tbest = t;
+          best = ref;
+        }
+      }
+    }
+    if (sp == 0) break;
+    --sp;
+    todo = stk[sp * 64];
+  }
+  return best;
+}
+
+// ---------------------------------------------------------------------------------------
+// Textures (texture.hpp:34-151, perlin.hpp:95-158, 219-255)
+__device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
+  const float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
+  const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+  const int i = static_cast<int>(fx), j = static_cast<int>(fy), k = static_cast<int>(fz);
+  const float uu = u * u * (3.0f - 2.0f * u);
+  const float vv = v * v * (3.0f - 2.0f * v);
+  const float ww = w * w * (3.0f - 2.0f * w);
+  float accum = 0.0f;
+#pragma unroll
+  for (int di = 0; di < 2; ++di) {
+#pragma unroll
+    for (int dj = 0; dj < 2; ++dj) {
+#pragma unroll
+      for (int dk = 0; dk < 2; ++dk) {
+        const int idx = perm[(i + di) & 255] ^ perm[256 + ((j + dj) & 255)] ^
+                        perm[512 + ((k + dk) & 255)];
+        const V3 c = xyz(vec[idx]);
+        const V3 wv = v3(u - di, v - dj, w - dk);
+        const float fu = di ? uu : (1.0f - uu);
+        const float fv = dj ? vv : (1.0f - vv);
+        const float fw = dk ? ww : (1.0f - ww);
+        accum += fu * fv * fw * dot(c, wv);
+      }
+    }
+  }
+  return accum;
+}
+
+__device__ float perlin_turb(const float4* vec, const int32_t* perm, V3 p) {
+  float accum = 0.0f, weight = 1.0f;
+  V3 tp = p;
+  for (int i = 0; i < 7; ++i) {
+    accum += weight * perlin_noise(vec, perm, tp);
+    weight *= 0.5f;
+    tp = scl(2.0f, tp);
+  }
+  return fabsf(accum);
+}
+
+__device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3 p) {
+  for (int guard = 0; guard < kMaxTexNesting; ++guard) {
+    const float4 t0 = S.textures[tex * 2];
+    const float4 t1 = S.textures[tex * 2 + 1];
+    const int type = ibits(t0.x);
+    if (type == RTG_TEX_SOLID) return xyz(t1);
+    if (type == RTG_TEX_CHECKER) {
+      const float inv_scale = t0.w;
+      const int xi = static_cast<int>(floorf(inv_scale * p.x));
+      const int yi = static_cast<int>(floorf(inv_scale * p.y));
+      const int zi = static_cast<int>(floorf(inv_scale * p.z));
+      const bool even = ((xi + yi + zi) % 2) == 0;
+      tex = even ? ibits(t0.y) : ibits(t0.z);
+      continue;
+    }
+    if (type == RTG_TEX_IMAGE) {
+      const int img = ibits(t1.w);
+      if (img < 0) return v3(0.0f, 1.0f, 1.0f);
+      const int4 h = S.images[img];
+      if (h.y <= 0) return v3(0.0f, 1.0f, 1.0f);
+      const float uc = fminf(fmaxf(u, 0.0f), 1.0f);
+      const float vc = 1.0f - fminf(fmaxf(v, 0.0f), 1.0f);
+      int i = static_cast<int>(uc * static_cast<float>(h.x));
+      int j = static_cast<int>(vc * static_cast<float>(h.y));
+      i = i < 0 ? 0 : (i < h.x ? i : h.x - 1);
+      j = j < 0 ? 0 : (j < h.y ? j : h.y - 1);
+      const uint64_t off = (static_cast<uint64_t>(static_cast<uint32_t>(h.w)) << 32) |
+                           static_cast<uint32_t>(h.z);
+      const uint8_t* px = S.texels + off + (static_cast<int64_t>(j) * h.x + i) * 3;
+      const float cs = 1.0f / 255.0f;
+      return v3(cs * px[0], cs * px[1], cs * px[2]);
+    }
+    if (type == RTG_TEX_NOISE) {
+      const int pt = ibits(t1.w);
+      const float4* vec = S.perlin_vec + pt * 256;
+      const int32_t* perm = S.perlin_perm + pt * 768;
+      const float t = perlin_turb(vec, perm, p);
+      const float s = 0.5f * (1.0f + sinf(t0.w * p.z + 10.0f * t));
+      return v3(s, s, s);
+    }
+    break;
+  }
+  return v3(1.0f, 0.0f, 1.0f);
+}
+
+// ---------------------------------------------------------------------------------------
+struct PathState {
+  V3 o, d;
+  float time;
+  V3 T, L;
+  int depth;
+  uint64_t rng;
+};
+
+// get_ray (camera.hpp:139-177): jitter x then y, lens disk (rejection), time.
+__device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, uint64_t seed_mix,
+                                             uint32_t pixel_id, uint32_t sample, int i, int j) {
+  ps.rng = mix64(((static_cast<uint64_t>(pixel_id) << 32) | sample) ^ seed_mix);
+  const float ox = uniform(ps.rng) - 0.5f;
+  const float oy = uniform(ps.rng) - 0.5f;
+  const float fi = static_cast<float>(i) + ox;
+  const float fj = static_cast<float>(j) + oy;
+  const V3 p00 = v3(C.pixel00[0], C.pixel00[1], C.pixel00[2]);
+  const V3 du = v3(C.du[0], C.du[1], C.du[2]);
+  const V3 dv = v3(C.dv[0], C.dv[1], C.dv[2]);
+  const V3 sample_pt = add(add(p00, scl(fi, du)), scl(fj, dv));
+  V3 origin = v3(C.center[0], C.center[1], C.center[2]);
+  if (C.defocus) {
+    float px = 0.0f, py = 0.0f;
+    for (int k = 0; k < kMaxRejectTries; ++k) {
+      const float x = uniform_m11(ps.rng);
+      const float y = uniform_m11(ps.rng);
+      if (x * x + y * y < 1.0f) {
+        px = x;
+        py = y;
+        break;
+      }
+    }
+    origin = add(add(origin, scl(px, v3(C.defu[0], C.defu[1], C.defu[2]))),
+                 scl(py, v3(C.defv[0], C.defv[1], C.defv[2])));
+  }
+  ps.o = origin;
+  ps.d = sub(sample_pt, origin);
+  ps.time = uniform(ps.rng);
+  ps.T = v3(1.0f, 1.0f, 1.0f);
+  ps.L = v3(0.0f, 0.0f, 0.0f);
+  ps.depth = C.max_depth;
+}
+
+// Shades the closest hit `ref` at distance t; returns false when the path ends
+// (ray_color's emission-only return, camera.hpp:213-216, or a miss handled by the caller).
+__device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
+  V3 p, outward;
+  float u = 0.0f, v = 0.0f;
+  int mat;
+  bool sphere = !(ref & kQuadRefBit);
+  if (sphere) {
+    const float4* s = S.spheres + static_cast<int64_t>(ref) * 2;
+    const float4 s0 = s[0], s1 = s[1];
+    const V3 C = v3(s0.x + ps.time * s1.x, s0.y + ps.time * s1.y, s0.z + ps.time * s1.z);
+    p = add(ps.o, scl(t, ps.d));
+    outward = scl(1.0f / s0.w, sub(p, C));
+    mat = ibits(s1.w);
+  } else {
+    const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
+    const float4 q0 = q[0];
+    p = add(ps.o, scl(t, ps.d));
+    const V3 hp = sub(p, xyz(q0));
+    const V3 w = xyz(q[3]);
+    u = dot(w, cross(hp, xyz(q[2])));
+    v = dot(w, cross(xyz(q[1]), hp));
+    outward = xyz(q[4]);
+    mat = ibits(q[1].w);
+  }
+  const bool front = dot(ps.d, outward) < 0.0f;  // set_face_normal, hittable.hpp:29-35
+  const V3 n = front ? outward : neg(outward);
+  const float4 m0 = S.materials[mat * 2];
+  const float4 m1 = S.materials[mat * 2 + 1];
+  const int type = ibits(m0.x);
+  const int tex = ibits(m0.y);
+  const bool needs_uv = sphere && ibits(m1.w) != 0;  // texture (transitively) is an image
+
+  // texture coordinates on spheres are only consumed by image textures
+  auto sphere_uv = [&]() {
+    const float theta = acosf(-outward.y);
+    const float phi = atan2f(-outward.z, outward.x) + kPi;
+    u = phi / (2.0f * kPi);
+    v = theta / kPi;
+  };
+
+  if (type == RTG_MAT_DIFFUSE_LIGHT) {
+    if (needs_uv) sphere_uv();
+    const V3 e = texture_value(S, tex, u, v, p);
+    ps.L = add(ps.L, mul(ps.T, e));
+    return false;
+  }
+  V3 dir, att;
+  if (type == RTG_MAT_LAMBERTIAN) {
+    const V3 r = random_unit_vector(ps.rng);
+    dir = add(n, r);
+    // near_zero with the reference's fabs(e[1] < s) quirk (vec3.hpp:70-77, H5)
+    const float s = 1e-8f;
+    if (fabsf(dir.x) < s && dir.y < s && fabsf(dir.z) < s) dir = n;
+    if (needs_uv) sphere_uv();
+    att = texture_value(S, tex, u, v, p);
+  } else if (type == RTG_MAT_METAL) {
+    const V3 in = ps.d;
+    const V3 refl = sub(in, scl(2.0f * dot(in, n), n));
+    const V3 r = random_unit_vector(ps.rng);
+    dir = add(unit(refl), scl(m0.z, r));
+    att = xyz(m1);
+    if (!(dot(dir, n) > 0.0f)) return false;  // absorbed: color_from_emission == 0
+  } else if (type == RTG_MAT_DIELECTRIC) {
+    att = v3(1.0f, 1.0f, 1.0f);
+    const float eta = m0.w;
+    const float ri = front ? (1.0f / eta) : eta;
+    const V3 ud = unit(ps.d);
+    const float cos_t = fminf(dot(neg(ud), n), 1.0f);
+    const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+    const bool cannot = ri * sin_t > 1.0f;
+    bool reflect = cannot;
+    if (!cannot) {
+      float r0 = (1.0f - ri) / (1.0f + ri);
+      r0 = r0 * r0;
+      const float x = 1.0f - cos_t;
+      const float refl = r0 + (1.0f - r0) * (x * x * x * x * x);
+      reflect = refl > uniform(ps.rng);
+    }
+    if (reflect) {
+      dir = sub(ud, scl(2.0f * dot(ud, n), n));
+    } else {
+      const float ct = fminf(dot(neg(ud), n), 1.0f);
+      const V3 perp = scl(ri, add(ud, scl(ct, n)));
+      const V3 par = scl(-sqrtf(fabsf(1.0f - dot(perp, perp))), n);
+      dir = add(perp, par);
+    }
+  } else {
+    return false;  // base material: scatter() == false, emitted() == 0
+  }
+  ps.T = mul(ps.T, att);
+  ps.o = p;
+  ps.d = dir;
+  return true;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+template <int STACK, bool COUNT>
+__global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
+  __shared__ int32_t s_stack[4 * STACK * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int32_t* stk = s_stack + wave * STACK * 64 + lane;
+  const int i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+  const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  const bool valid = i < C.width && lr < J.row_count;
+  const int j = J.row_begin + lr * J.row_stride;
+  const uint32_t pixel_id = static_cast<uint32_t>(j) * static_cast<uint32_t>(C.width) +
+                            static_cast<uint32_t>(i);
+
+  V3 acc = v3(0.0f, 0.0f, 0.0f);
+  uint32_t segs = 0, hits = 0;
+  Counts<COUNT> cnt;
+  bool overflow = false;
+  int sample = (valid && C.max_depth > 0) ? 0 : C.spp;
+  PathState ps;
+  if (sample < C.spp) start_sample(ps, C, J.seed_mix, pixel_id, 0, i, j);
+  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
+  while (sample < C.spp) {
+    float t = __builtin_inff();
+    const int32_t ref = closest_hit<STACK, COUNT>(S, ps.o, ps.d, ps.time, t, stk, cnt, overflow);
+    ++segs;
+    bool alive;
+    if (ref < 0) {
+      ps.L = add(ps.L, mul(ps.T, bg));
+      alive = false;
+    } else {
+      if (COUNT) ++hits;
+      alive = shade(S, ps, ref, t);
+      if (alive && --ps.depth <= 0) alive = false;
+    }
+    if (!alive) {
+      acc = add(acc, ps.L);
+      ++sample;
+      if (sample < C.spp) start_sample(ps, C, J.seed_mix, pixel_id, sample, i, j);
+    }
+  }
+  if (valid) {
+    float* o = J.out + (static_cast<int64_t>(lr) * C.width + i) * 3;
+    o[0] = C.scale * acc.x;
+    o[1] = C.scale * acc.y;
+    o[2] = C.scale * acc.z;
+  }
+  const uint32_t wsegs = wave_sum(segs);
+  if (COUNT) {
+    const uint32_t wbox = wave_sum(cnt.box);
+    const uint32_t wprim = wave_sum(cnt.prim);
+    const uint32_t whits = wave_sum(hits);
+    if (lane == 0) {
+      atomicAdd(&J.counters[1], static_cast<unsigned long long>(wbox));
+      atomicAdd(&J.counters[2], static_cast<unsigned long long>(wprim));
+      atomicAdd(&J.counters[3], static_cast<unsigned long long>(whits));
+    }
+  }
+  if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
+  if (__any(overflow) && lane == 0) atomicAdd(&J.counters[4], 1ull);
+}
+
+// write_color (color.hpp:14-58): sqrt gamma, clamp to [0, 0.999], int(256 * x).
+__global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ in,
+                                                      uint8_t* __restrict__ out, int64_t n) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n * 3) return;
+  float x = in[k];
+  x = x > 0.0f ? sqrtf(x) : 0.0f;
+  x = x < 0.0f ? 0.0f : (x > 0.999f ? 0.999f : x);
+  out[k] = static_cast<uint8_t>(static_cast<int>(256.0f * x));
+}
+
+template <int STACK>
+hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
+                        hipStream_t stream) {
+  const dim3 block(256);
+  const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
+  if (count) {
+    hipLaunchKernelGGL((render_kernel<STACK, true>), grid, block, 0, stream, S, C, J);
+  } else {
+    hipLaunchKernelGGL((render_kernel<STACK, false>), grid, block, 0, stream, S, C, J);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int kernel_stack_depth(int bvh_depth) {
+  if (bvh_depth <= 16) return 16;
+  if (bvh_depth <= 32) return 32;
+  if (bvh_depth <= 64) return 64;
+  return -1;
+}
+
+hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
+                         bool count, hipStream_t stream) {
+  if (J.row_count <= 0 || C.width <= 0) return hipSuccess;
+  switch (stack) {
+    case 16:
+      return launch_stack<16>(S, C, J, count, stream);
+    case 32:
+      return launch_stack<32>(S, C, J, count, stream);
+    case 64:
+      return launch_stack<64>(S, C, J, count, stream);
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream) {
+  if (n_pixels <= 0) return hipSuccess;
+  const int64_t total = n_pixels * 3;
+  const unsigned blocks = static_cast<unsigned>((total + 255) / 256);
+  hipLaunchKernelGGL(resolve_kernel, dim3(blocks), dim3(256), 0, stream, in, out, n_pixels);
+  return hipGetLastError();
+}
+
+}  // namespace rtg

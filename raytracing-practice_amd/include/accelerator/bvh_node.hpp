@@ -1,0 +1,74 @@
+// accelerator/bvh_node.hpp — host BVH node with the reference's topology (bvh_node.hpp:16-134):
+// longest axis of the range box, std::sort by bbox.min on that axis, split at the median.
+// On the device the library builds its own BVH over the flattened primitives (RTG_BVH_MEDIAN
+// reproduces this topology, RTG_BVH_SAH is the fast default); flattening a bvh_node therefore
+// emits the objects in the order of the list it was built from (the root keeps that order), so
+// the flat scene lists objects exactly as the reference's hittable_list did.
+#pragma once
+#include <algorithm>
+
+#include "accelerator/aabb.hpp"
+#include "hittable/hittable.hpp"
+#include "hittable/hittable_list.hpp"
+
+class bvh_node : public hittable {
+ public:
+  bvh_node(hittable_list list) : bvh_node(list.objects, 0, list.objects.size(), list.objects) {}
+
+  bvh_node(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end) {
+    build(objects, start, end);
+  }
+
+ private:
+  // root only: the unsorted object list, in insertion order
+  bvh_node(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end,
+           std::vector<std::shared_ptr<hittable>> original)
+      : list_order(std::move(original)) {
+    build(objects, start, end);
+  }
+
+  void build(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end) {
+    bbox = aabb::empty;
+    for (size_t i = start; i < end; ++i) bbox = aabb(bbox, objects[i]->bounding_box());
+    const int axis = bbox.longest_axis();
+    const size_t span = end - start;
+    if (span == 1) {
+      left = right = objects[start];
+    } else if (span == 2) {
+      left = objects[start];
+      right = objects[start + 1];
+    } else {
+      std::sort(objects.begin() + start, objects.begin() + end,
+                [axis](const std::shared_ptr<hittable>& a, const std::shared_ptr<hittable>& b) {
+                  return a->bounding_box().axis_interval(axis).min < b->bounding_box().axis_interval(axis).min;
+                });
+      const size_t mid = start + span / 2;
+      left = std::make_shared<bvh_node>(objects, start, mid);
+      right = std::make_shared<bvh_node>(objects, mid, end);
+    }
+  }
+
+ public:
+  bool hit(const ray& r, interval ray_t, hit_record& rec) const override {
+    if (!bbox.hit(r, ray_t)) return false;
+    const bool hl = left->hit(r, ray_t, rec);
+    const bool hr = right->hit(r, interval(ray_t.min, hl ? rec.t : ray_t.max), rec);
+    return hl || hr;
+  }
+  aabb bounding_box() const override { return bbox; }
+
+  bool rtg_flatten(rtgpu::scene_builder& sb, const vec3& offset) const override {
+    if (!list_order.empty()) {
+      for (const auto& obj : list_order)
+        if (!obj->rtg_flatten(sb, offset)) return false;
+      return true;
+    }
+    if (!left->rtg_flatten(sb, offset)) return false;
+    return right == left || right->rtg_flatten(sb, offset);
+  }
+
+ private:
+  std::vector<std::shared_ptr<hittable>> list_order;
+  std::shared_ptr<hittable> left, right;
+  aabb bbox;
+};

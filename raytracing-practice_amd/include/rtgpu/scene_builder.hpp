@@ -1,0 +1,78 @@
+// rtgpu/scene_builder.hpp — flattens the C++ object graph (hittable / material / texture, all
+// shared_ptr-linked as in the reference) into the flat arrays of rtg_scene_desc (include/rtgpu.h).
+// Materials, textures, images and perlin tables are de-duplicated by object identity, so a
+// texture shared by many spheres (e.g. main.cpp:180-183) is uploaded once.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rtgpu.h"
+
+class material;
+class texture;
+
+namespace rtgpu {
+
+class scene_builder {
+ public:
+  std::vector<rtg_primitive> prims;
+  std::vector<rtg_material> materials;
+  std::vector<rtg_texture> textures;
+  std::vector<rtg_image> images;
+  std::vector<std::shared_ptr<const std::vector<uint8_t>>> image_bytes;
+  std::vector<rtg_perlin> perlins;
+  std::string error;
+
+  // Index of the flattened material / texture (exports on first use); -1 on failure.
+  int32_t material_id(const material* m);  // defined in core/material.hpp
+  int32_t texture_id(const texture* t);    // defined in core/texture.hpp
+  enum memo_kind { kMaterial = 0, kTexture = 1, kImage = 2, kPerlin = 3 };
+
+  int32_t image_id(const void* key, int w, int h, std::shared_ptr<const std::vector<uint8_t>> rgb) {
+    auto& memo = memo_table(kImage);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+    rtg_image im{w, h, rgb ? rgb->data() : nullptr};
+    images.push_back(im);
+    image_bytes.push_back(rgb);
+    return memo[key] = static_cast<int32_t>(images.size() - 1);
+  }
+  int32_t perlin_id(const void* key, const rtg_perlin& p) {
+    auto& memo = memo_table(kPerlin);
+    auto it = memo.find(key);
+    if (it != memo.end()) return it->second;
+    perlins.push_back(p);
+    return memo[key] = static_cast<int32_t>(perlins.size() - 1);
+  }
+  bool fail(const std::string& what) {
+    if (error.empty()) error = what;
+    return false;
+  }
+  // identity -> index table, one per exported object kind
+  std::map<const void*, int32_t>& memo_table(memo_kind k) { return memo_[k]; }
+
+  rtg_scene_desc desc(int32_t bvh_mode) const {
+    rtg_scene_desc d{};
+    d.abi_version = RTG_ABI_VERSION;
+    d.bvh_mode = bvh_mode;
+    d.prims = prims.data();
+    d.num_prims = static_cast<int64_t>(prims.size());
+    d.materials = materials.data();
+    d.num_materials = static_cast<int32_t>(materials.size());
+    d.textures = textures.data();
+    d.num_textures = static_cast<int32_t>(textures.size());
+    d.images = images.data();
+    d.num_images = static_cast<int32_t>(images.size());
+    d.perlins = perlins.data();
+    d.num_perlins = static_cast<int32_t>(perlins.size());
+    return d;
+  }
+
+ private:
+  std::map<const void*, int32_t> memo_[4];
+};
+
+}  // namespace rtgpu

@@ -1,0 +1,69 @@
+"""Pins the oracle's renderers as whole loops.
+
+* cpu_ref64 (the reference algorithm, glibc stream, fp64) must reproduce the "ref-hybrid" render
+  of tests/golden/hybrid_*.npz — produced by the reference's geometry / BVH / RNG / perlin code
+  with a restated camera+material loop (oracle/ref_harness.cpp) — bit for bit, segment for segment.
+* cpu_ref32 (the fp32 spec the GPU implements, counter RNG) must agree with cpu_ref64 in
+  distribution: same expected image, different random numbers (hazard H1 makes per-pixel
+  agreement with the reference's global rand() stream impossible).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import rtgpu
+from conftest import GOLDEN
+
+SCENE_OF = {"book1": "bouncing_spheres", "cornell": "cornell_box", "simple_light": "simple_light",
+            "perlin": "perlin_sphere"}
+
+
+def hybrid_camera(scene, W, H, spp, depth):
+    """setup_cam() of oracle/ref_harness.cpp (the reference cameras of main.cpp)."""
+    kw = dict(image_width=W, aspect_ratio=W / H, samples_per_pixel=spp, max_depth=depth,
+              background=(0.7, 0.8, 1.0), vfov=20.0, lookfrom=(13, 2, 3), lookat=(0, 0, 0),
+              vup=(0, 1, 0), defocus_angle=0.0, focus_dist=10.0)
+    kw["background"] = tuple(float(np.float32(x)) for x in kw["background"])
+    if scene == "book1":
+        kw["defocus_angle"] = float(np.float32(0.6))
+    elif scene == "cornell":
+        kw.update(background=(0, 0, 0), vfov=40.0, lookfrom=(278, 278, -800), lookat=(278, 278, 0))
+    elif scene == "simple_light":
+        kw.update(background=(0, 0, 0), lookfrom=(26, 3, 6), lookat=(0, 2, 0))
+    return rtgpu.camera(**kw)
+
+
+@pytest.mark.parametrize("scene", sorted(SCENE_OF))
+def test_cpu_ref64_reproduces_reference_render(scenes, oracle, scene):
+    z = np.load(os.path.join(GOLDEN, f"hybrid_{scene}.npz"))
+    W, H, spp, depth, seed = (int(z[k]) for k in ("W", "H", "spp", "depth", "seed"))
+    s = scenes.build(SCENE_OF[scene], rand_seed=1)
+    cam = hybrid_camera(scene, W, H, spp, depth)
+    fb, segs = oracle.render_f64(s.desc, cam, seed=seed)
+    assert segs == int(z["segments"])
+    assert np.array_equal(fb, z["fb"]), f"max |diff| {np.abs(fb - z['fb']).max()}"
+
+
+@pytest.mark.parametrize("scene,spp", [("book1", 64), ("cornell", 128), ("simple_light", 64)])
+def test_cpu_ref32_matches_ref64_in_distribution(scenes, oracle, scene, spp):
+    """cpu_ref32 differs from cpu_ref64 by no more than two independent cpu_ref64 runs differ from
+    each other (block means of 4x4 pixels), i.e. fp32 + the counter RNG change the noise, not the
+    expected image."""
+    W, H = (48, 27) if scene != "cornell" else (24, 24)
+    s = scenes.build(SCENE_OF[scene], rand_seed=1)
+    cam = hybrid_camera(scene, W, H, spp, 20)
+    f32, seg32 = oracle.render_f32(s.desc, cam, seed=rtgpu.DEFAULT_SEED)
+    fa, sega = oracle.render_f64(s.desc, cam, seed=12345)
+    fb, _ = oracle.render_f64(s.desc, cam, seed=777)
+    assert abs(seg32 - sega) / sega < 0.02  # same mean path length
+    b = 4
+    hb, wb = H // b, W // b
+
+    def blocks(x):
+        return x[:hb * b, :wb * b].astype(np.float64).reshape(hb, b, wb, b, 3).mean(axis=(1, 3))
+
+    d_spec = np.abs(blocks(f32) - blocks(fa)).mean()
+    d_noise = np.abs(blocks(fb) - blocks(fa)).mean()
+    assert d_spec < 1.35 * d_noise + 1e-4, (d_spec, d_noise)
+    assert abs(float(f32.mean()) - float(fa.mean())) < 3 * d_noise / np.sqrt(hb * wb)

@@ -255,6 +255,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     const BuildNode& n = bvh.nodes[k];
     float lo[2][3], hi[2][3];
     int32_t code[2];
+    if (n.child[0] == kEmptyChild) {  // the kernel only guards the right slot
+      *err = "BVH node with an empty left child";
+      return false;
+    }
     for (int s = 0; s < 2; ++s) {
       if (n.child[s] == kEmptyChild) {
         for (int a = 0; a < 3; ++a) {
@@ -544,6 +548,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.perlin_vec = reinterpret_cast<const float4*>(base + parts[8].off);
   s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
   s->dev.num_nodes = hs.num_nodes;
+  s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
 
   s->info.device = device;
   s->info.bvh_mode = desc->bvh_mode;
@@ -586,6 +591,7 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   const unsigned long long* c = s->host_counters;
   s->pending = false;
   if (c[4] != 0) return fail(RTG_E_UNSUPPORTED, "BVH traversal stack overflow");
+  if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
   if (stats) {
     stats->segments = c[0];
     stats->box_tests = c[1];

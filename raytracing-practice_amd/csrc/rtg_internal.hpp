@@ -92,6 +92,7 @@ struct DevScene {
   const float4* perlin_vec;
   const int32_t* perlin_perm;
   int64_t num_nodes;
+  int64_t num_refs;
 };
 
 struct DevJob {
@@ -101,7 +102,8 @@ struct DevJob {
   int32_t row_count;
   int32_t pad_;
   float* out;
-  unsigned long long* counters;  // [0] segments, [1] box tests, [2] prim tests, [3] hits
+  // [0] segments, [1] box tests, [2] prim tests, [3] hits, [4] stack overflow, [5] bad BVH code
+  unsigned long long* counters;
 };
 
 }  // namespace rtg

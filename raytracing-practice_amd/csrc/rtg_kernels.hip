@@ -148,7 +148,7 @@ struct Counts {
 template <int STACK, bool COUNT>
 __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, float time,
                                                float& tbest, int32_t* stk, Counts<COUNT>& cnt,
-                                               bool& overflow) {
+                                               bool& overflow, bool& corrupt) {
   int32_t best = -1;
   if (S.num_nodes == 0) return best;
   const V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y),
@@ -158,6 +158,10 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
   int32_t todo = 0;
   while (true) {
     if (todo >= 0) {
+      if (todo >= S.num_nodes) {  // corrupt child code: report, never read out of bounds
+        corrupt = true;
+        break;
+      }
       const float4* n = S.nodes + static_cast<int64_t>(todo) * 4;
       const float4 a = n[0], b = n[1], c = n[2];
       const int4 ch = *reinterpret_cast<const int4*>(n + 3);
@@ -173,8 +177,11 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
       const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tbest));
       const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kTMin));
       const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tbest));
+      // An empty slot (right child only; the host guarantees the left one is never empty) has an
+      // inverted box, which the symmetric min/max slab form would report as all of space: test
+      // the child code explicitly.
       const bool hl = ln <= lf;
-      const bool hr = rn <= rf;
+      const bool hr = rn <= rf && ch.y != kEmptyChild;
       if (hl && hr) {
         const bool lfirst = ln <= rn;
         const int32_t nearc = lfirst ? ch.x : ch.y;
@@ -196,6 +203,10 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
       const int32_t code = ~todo;
       const int32_t first = code >> 3;
       const int32_t count = (code & 7) + 1;
+      if (static_cast<int64_t>(first) + count > S.num_refs) {
+        corrupt = true;
+        break;
+      }
       for (int k = 0; k < count; ++k) {
         const int32_t ref = S.refs[first + k];
         float t;
@@ -467,14 +478,15 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   V3 acc = v3(0.0f, 0.0f, 0.0f);
   uint32_t segs = 0, hits = 0;
   Counts<COUNT> cnt;
-  bool overflow = false;
+  bool overflow = false, corrupt = false;
   int sample = (valid && C.max_depth > 0) ? 0 : C.spp;
   PathState ps;
   if (sample < C.spp) start_sample(ps, C, J.seed_mix, pixel_id, 0, i, j);
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   while (sample < C.spp) {
     float t = __builtin_inff();
-    const int32_t ref = closest_hit<STACK, COUNT>(S, ps.o, ps.d, ps.time, t, stk, cnt, overflow);
+    const int32_t ref =
+        closest_hit<STACK, COUNT>(S, ps.o, ps.d, ps.time, t, stk, cnt, overflow, corrupt);
     ++segs;
     bool alive;
     if (ref < 0) {
@@ -510,6 +522,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   }
   if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
   if (__any(overflow) && lane == 0) atomicAdd(&J.counters[4], 1ull);
+  if (__any(corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
 }
 
 // write_color (color.hpp:14-58): sqrt gamma, clamp to [0, 0.999], int(256 * x).

@@ -34,12 +34,18 @@ def compare(gpu_lib, scenes, oracle, name, seed=rtgpu.DEFAULT_SEED, bvh=rtgpu.RT
 
 
 def assert_parity(g, o, st, segs, exact_frac=0.999):
+    """RMSE < 1e-3 is the bar. Beyond it: scenes without transcendental textures must match the
+    oracle bit for bit on >= exact_frac of the pixels; textured scenes (sinf / acosf / atan2f may
+    differ by an ulp between ocml and glibc) must match within 1e-5 on >= 99.9 % of the pixels."""
     assert g.shape == o.shape
     assert np.all(np.isfinite(g))
     e = rmse(g, o)
     assert e < RMSE_TOL, e
-    frac = float(np.mean(np.all(g == o, axis=-1)))
-    assert frac >= exact_frac, (frac, e)
+    if exact_frac >= 0.999:
+        frac = float(np.mean(np.all(g == o, axis=-1)))
+    else:
+        frac = float(np.mean(np.all(np.abs(g - o) <= 1e-5, axis=-1)))
+    assert frac >= 0.999, (frac, e)
     assert abs(int(st.segments) - int(segs)) <= max(2, 1e-4 * segs), (st.segments, segs)
 
 
@@ -57,10 +63,10 @@ def test_book1_config1(gpu_lib, scenes, oracle):
     ("cornell_box", 96, 16, 50, 0.999),
     ("quads", 64, 8, 50, 0.999),
     ("checkered_spheres", 96, 8, 20, 0.999),
-    ("simple_light", 96, 8, 50, 0.95),     # noise texture: sinf may differ by an ulp
-    ("perlin_sphere", 96, 8, 50, 0.95),
-    ("earth", 96, 8, 50, 0.95),            # image texture: acosf/atan2f ulps can move a texel
-    ("earth_perlin", 96, 8, 50, 0.95),
+    ("simple_light", 96, 8, 50, 0.0),      # noise texture: sinf may differ by an ulp
+    ("perlin_sphere", 96, 8, 50, 0.0),
+    ("earth", 96, 8, 50, 0.0),             # image texture: acosf/atan2f ulps can move a texel
+    ("earth_perlin", 96, 8, 50, 0.0),
 ])
 def test_reference_scenes(gpu_lib, scenes, oracle, name, W, spp, depth, exact):
     g, o, st, segs = compare(gpu_lib, scenes, oracle, name, image_width=W,

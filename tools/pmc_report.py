@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""tools/pmc_report.py — turn the rocprofv3 PMC CSVs of tools/profile.sh into per-launch metrics
+of the render kernel and (with --write-traffic) profiles/pmc_traffic.json, which bench.py reports
+as roofline.traffic.
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KB; on gfx950
+FETCH_SIZE counts half of a wide coalesced read stream, so it is doubled; WRITE_SIZE is exact for
+16-B-per-lane stores (the framebuffer stores here are 4 B per lane: uncalibrated, reported as is).
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def load(path, kernel_filter):
+    per = collections.defaultdict(dict)
+    meta = {}
+    for r in csv.DictReader(open(path)):
+        if kernel_filter not in r["Kernel_Name"]:
+            continue
+        d = int(r["Dispatch_Id"])
+        per[d][r["Counter_Name"]] = per[d].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        meta[d] = (r["Kernel_Name"], int(r["VGPR_Count"]), int(r["LDS_Block_Size"]),
+                   int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return per, meta
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof_dir", nargs="?", default="gpurun_out/prof")
+    ap.add_argument("--kernel", default="render_kernel<")
+    ap.add_argument("--timed-only", action="store_true", default=True,
+                    help="use the non-counting dispatches only")
+    ap.add_argument("--workload", default=None)
+    ap.add_argument("--write-traffic", default=None)
+    a = ap.parse_args()
+    counters, info = {}, {}
+    for sub in sorted(os.listdir(a.prof_dir)):
+        p = os.path.join(a.prof_dir, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        per, meta = load(p, a.kernel)
+        for d, vals in per.items():
+            name = meta[d][0]
+            if a.timed_only and ", true>" in name:
+                continue  # RTG_RENDER_COUNT variant
+            for k, v in vals.items():
+                counters.setdefault(k, []).append(v)
+            info[sub] = meta[d]
+    avg = {k: sum(v) / len(v) for k, v in counters.items()}
+    out = {"per_launch": {k: avg[k] for k in sorted(avg)}}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        out["hbm_read_bytes"] = 2 * avg["FETCH_SIZE"] * 1024
+        out["hbm_write_bytes"] = avg["WRITE_SIZE"] * 1024
+        out["hbm_bytes_per_launch"] = out["hbm_read_bytes"] + out["hbm_write_bytes"]
+    if "SQ_THREAD_CYCLES_VALU" in avg and "SQ_ACTIVE_INST_VALU" in avg:
+        out["valu_lane_utilization"] = avg["SQ_THREAD_CYCLES_VALU"] / (64 * avg["SQ_ACTIVE_INST_VALU"])
+    if "SQ_WAVE_CYCLES" in avg:
+        w = avg["SQ_WAVE_CYCLES"]
+        out["wave_cycle_split"] = {k: avg[k] / w for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                                                          "SQ_ACTIVE_INST_ANY") if k in avg}
+    if "TCC_HIT_sum" in avg:
+        out["l2_hit_rate"] = avg["TCC_HIT_sum"] / max(1.0, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+    if "TCP_TOTAL_CACHE_ACCESSES_sum" in avg and "TCP_TCC_READ_REQ_sum" in avg:
+        out["l1_to_l2_read_fraction"] = avg["TCP_TCC_READ_REQ_sum"] / avg["TCP_TOTAL_CACHE_ACCESSES_sum"]
+    if "GRBM_GUI_ACTIVE" in avg:
+        ns = [m[3] for m in info.values()]
+        out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / (sum(ns) / len(ns))
+    out["dispatch"] = {k: {"vgpr": v[1], "lds": v[2], "ns": v[3]} for k, v in info.items()}
+    print(json.dumps(out, indent=1))
+    if a.write_traffic and "hbm_bytes_per_launch" in out:
+        with open(a.write_traffic, "w") as f:
+            json.dump({"workload": a.workload, "hbm_bytes_per_launch": int(out["hbm_bytes_per_launch"]),
+                       "hbm_read_bytes": int(out["hbm_read_bytes"]),
+                       "hbm_write_bytes": int(out["hbm_write_bytes"]),
+                       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                                 "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM"}, f, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

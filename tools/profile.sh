@@ -20,7 +20,7 @@ run() {  # name timeout rocprofv3-args...
   tail -n 4 "$OUT/$name.log"
   return $rc
 }
-run trace 600 --kernel-trace --stats -S --summary-output-file "$OUT/trace_summary.txt" \
+run trace 600 --kernel-trace --stats -S --summary-output-file summary \
     -f csv -d "$OUT/trace" -o run -- "${BENCH[@]}" || exit $?
 run pmc_fetch 600 --pmc FETCH_SIZE -f csv -d "$OUT/pmc_fetch" -o run -- "${PMC_BENCH[@]}" || exit $?
 run pmc_write 600 --pmc WRITE_SIZE -f csv -d "$OUT/pmc_write" -o run -- "${PMC_BENCH[@]}" || exit $?

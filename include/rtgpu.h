@@ -151,6 +151,14 @@ typedef struct rtg_camera_params {
 #define RTG_RENDER_OUT_DEVICE 0x1 /* out_rgb is a device pointer on the scene's device */
 #define RTG_RENDER_ASYNC 0x2      /* do not synchronize (requires OUT_DEVICE); stats filled later */
 #define RTG_RENDER_COUNT 0x4      /* also count box / primitive tests (slower, diagnostic) */
+/* Diagnostic schedule selection (A/B of kernel variants; 0 = the default everywhere):
+ * bits 8-15 schedule (0 default = 3 when the scene geometry fits in LDS else 4; 1 one closest-hit
+ * query per loop trip; 2 the first kernel; 3 persistent LDS-resident geometry, 12 waves per
+ * workgroup; 4 ballot-batched on a plain grid; 5 as 3 with 16 waves),
+ * bits 16-23 shade batch of schedule 0 in 64ths of the live lanes (0 = library default). */
+#define RTG_RENDER_SCHEDULE(n) (((n) & 0xff) << 8)
+#define RTG_RENDER_SHADE_BATCH(n) (((n) & 0xff) << 16)
+#define RTG_RENDER_LEAF_BATCH(n) (((n) & 0x7f) << 24) /* bits 24-30: leaf batch in lanes (0 = default) */
 
 typedef struct rtg_render_desc {
   uint64_t seed;      /* run seed of the counter RNG */
@@ -168,6 +176,11 @@ typedef struct rtg_render_stats {
   uint64_t prim_tests; /* RTG_RENDER_COUNT only: sphere/quad tests */
   uint64_t hits;       /* RTG_RENDER_COUNT only: segments that hit something */
   double kernel_ms;    /* device time of the render kernel (HIP events on the launch stream) */
+  /* RTG_RENDER_COUNT only, wave-level schedule diagnostics (default schedule):
+   * [0] traversal trips, [1] lanes stepping summed over trips, [2] lanes idle because their
+   * pixel is finished summed over trips, [3] shading trips, [4] lanes shading summed over trips,
+   * [5] / [6] shader-clock cycles spent in the traversal / shading phases (s_memtime, all waves) */
+  uint64_t diag[8];
 } rtg_render_stats;
 
 typedef struct rtg_scene rtg_scene; /* opaque; owns the device copy of the scene */

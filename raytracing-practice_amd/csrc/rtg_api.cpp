@@ -17,11 +17,19 @@
 namespace rtg {
 int kernel_stack_depth(int bvh_depth);
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
-                         bool count, hipStream_t stream);
+                         bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream);
+int lds_layout(const DevScene& S, int stack, int waves, DevJob* J);
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
 }  // namespace rtg
 
 using namespace rtg;
+
+namespace {
+constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
+constexpr int kDefaultLeafBatch = 16;   // lanes waiting at a leaf before a leaf trip
+constexpr int kDefaultLdsWaves = 12;    // persistent LDS workgroup size (schedule 3 = 12, 5 = 16)
+constexpr int kNumCounters = 16;        // [0..6] see DevJob::counters, [8..14] diagnostics
+}
 
 namespace {
 
@@ -383,6 +391,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
 
 struct rtg_scene {
   int device = 0;
+  int num_cus = 0;
   hipStream_t own_stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* dmem = nullptr;  // one allocation for all scene arrays
@@ -518,9 +527,9 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     return cleanup(hip_fail(e, "hipStreamCreate"));
   if ((e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess)
     return cleanup(hip_fail(e, "hipEventCreate"));
-  if ((e = hipMalloc(&s->counters, 8 * sizeof(unsigned long long))) != hipSuccess)
+  if ((e = hipMalloc(&s->counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return cleanup(hip_fail(e, "hipMalloc(counters)"));
-  if ((e = hipHostMalloc(&s->host_counters, 8 * sizeof(unsigned long long))) != hipSuccess)
+  if ((e = hipHostMalloc(&s->host_counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return cleanup(hip_fail(e, "hipHostMalloc(counters)"));
   char* base = static_cast<char*>(s->dmem);
   for (const Part& p : parts) {
@@ -549,6 +558,9 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
   s->dev.num_nodes = hs.num_nodes;
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
+  s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
+  s->dev.num_quads = static_cast<int64_t>(hs.quads.size() / 20);
+  s->num_cus = prop.multiProcessorCount;
 
   s->info.device = device;
   s->info.bvh_mode = desc->bvh_mode;
@@ -599,6 +611,7 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
     stats->hits = c[3];
     stats->samples = s->pending_samples;
     stats->kernel_ms = ms;
+    for (int k = 0; k < 8; ++k) stats->diag[k] = c[8 + k];
   }
   return RTG_OK;
 }
@@ -653,15 +666,30 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dj.row_begin = job->row_begin;
   dj.row_stride = job->row_stride;
   dj.row_count = rows;
+  const int batch = (job->flags >> 16) & 0xff;
+  dj.shade_batch = batch == 0 ? kDefaultShadeBatch : (batch > 64 ? 64 : batch);
+  const int leaf_batch = (job->flags >> 24) & 0x7f;
+  dj.leaf_batch = leaf_batch == 0 ? kDefaultLeafBatch : (leaf_batch > 64 ? 64 : leaf_batch);
   dj.out = dout;
+  dj.tiles_x = (W + 7) / 8;
+  dj.num_tiles = dj.tiles_x * ((rows + 7) / 8);
+  // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
+  int variant = (job->flags >> 8) & 0xff;
+  if (variant == 0) variant = lds_layout(s->dev, s->info.stack_depth, kDefaultLdsWaves, nullptr) > 0
+                                  ? (kDefaultLdsWaves == 16 ? 5 : 3) : 4;
+  const int lds_bytes = lds_layout(s->dev, s->info.stack_depth, variant == 5 ? 16 : 12, &dj);
+  if (variant == 4) variant = 0;  // plain-grid ballot schedule
+  if ((variant == 3 || variant == 5) && lds_bytes < 0)
+    return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
+  const int grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
   dj.counters = s->counters;
-  RTG_HIP(hipMemsetAsync(s->counters, 0, 8 * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
   RTG_HIP(launch_render(s->dev, dc, dj, s->info.stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
-                        stream),
+                        variant, lds_bytes, grid_blocks, stream),
           "render kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
-  RTG_HIP(hipMemcpyAsync(s->host_counters, s->counters, 8 * sizeof(unsigned long long),
+  RTG_HIP(hipMemcpyAsync(s->host_counters, s->counters, kNumCounters * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, stream),
           "hipMemcpyAsync(counters)");
   if (!dev_out) {

@@ -93,6 +93,8 @@ struct DevScene {
   const int32_t* perlin_perm;
   int64_t num_nodes;
   int64_t num_refs;
+  int64_t num_spheres;
+  int64_t num_quads;
 };
 
 struct DevJob {
@@ -100,10 +102,16 @@ struct DevJob {
   int32_t row_begin;
   int32_t row_stride;
   int32_t row_count;
-  int32_t pad_;
+  int32_t shade_batch;  // schedule 0: shade once ceil(alive * shade_batch / 64) lanes are ready
   float* out;
-  // [0] segments, [1] box tests, [2] prim tests, [3] hits, [4] stack overflow, [5] bad BVH code
+  // [0] segments, [1] box tests, [2] prim tests, [3] hits, [4] stack overflow, [5] bad BVH code,
+  // [6] persistent kernels' tile counter, [8..14] schedule diagnostics
   unsigned long long* counters;
+  int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
+  int32_t tiles_x;    // 8x8 pixel tiles per shard row of tiles
+  int32_t num_tiles;  // 8x8 pixel tiles in the shard
+  // persistent LDS kernel: byte offsets of the scene copies in dynamic LDS
+  int32_t lds_nodes, lds_refs, lds_spheres, lds_quads;
 };
 
 }  // namespace rtg

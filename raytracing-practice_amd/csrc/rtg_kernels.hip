@@ -142,6 +142,126 @@ struct Counts {
   uint32_t box = 0, prim = 0;
 };
 
+// Per-lane traversal state of the child-pair BVH (replaces hittable_list::hit -> bvh_node::hit
+// -> aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
+// traversal: the nearer child first, the farther one pushed on the lane's LDS stack.
+struct Trav {
+  V3 inv, oi;     // 1/d and -o/d for the fused slab test
+  float tbest;    // closest hit so far (the shrinking interval.max of the reference)
+  int32_t best;   // primitive ref of the closest hit, -1 = none
+  int32_t todo;   // node index (>= 0) or leaf code (< 0) to visit next
+  int32_t sp;     // stack depth
+  bool active;    // traversal not finished
+};
+
+__device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d) {
+  t.inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
+  t.oi = v3(-o.x * t.inv.x, -o.y * t.inv.y, -o.z * t.inv.z);
+  t.tbest = __builtin_inff();
+  t.best = -1;
+  t.todo = 0;
+  t.sp = 0;
+  t.active = S.num_nodes > 0;
+}
+
+__device__ __forceinline__ void trav_pop(Trav& t, int32_t* stk) {
+  if (t.sp == 0) {
+    t.active = false;
+    return;
+  }
+  --t.sp;
+  t.todo = stk[t.sp * 64];
+}
+
+// Visit one inner node (t.todo >= 0): test both child boxes, continue with the nearer hit child
+// and push the farther one, or pop when neither is hit.
+template <int STACK, bool COUNT>
+__device__ __forceinline__ void node_step(Trav& t, const DevScene& S, int32_t* stk, Counts<COUNT>& cnt,
+                                          bool& overflow, bool& corrupt) {
+  if (t.todo >= S.num_nodes) {  // corrupt child code: report, never read out of bounds
+    corrupt = true;
+    t.active = false;
+    return;
+  }
+  const float4* n = S.nodes + static_cast<int64_t>(t.todo) * 4;
+  const float4 a = n[0], b = n[1], c = n[2];
+  const int4 ch = *reinterpret_cast<const int4*>(n + 3);
+  if (COUNT) cnt.box += 2;
+  const V3 inv = t.inv, oi = t.oi;
+  // left box lo=(a.x,a.y,a.z) hi=(a.w,b.x,b.y); right lo=(b.z,b.w,c.x) hi=(c.y,c.z,c.w)
+  const float l0x = fmaf(a.x, inv.x, oi.x), l1x = fmaf(a.w, inv.x, oi.x);
+  const float l0y = fmaf(a.y, inv.y, oi.y), l1y = fmaf(b.x, inv.y, oi.y);
+  const float l0z = fmaf(a.z, inv.z, oi.z), l1z = fmaf(b.y, inv.z, oi.z);
+  const float r0x = fmaf(b.z, inv.x, oi.x), r1x = fmaf(c.y, inv.x, oi.x);
+  const float r0y = fmaf(b.w, inv.y, oi.y), r1y = fmaf(c.z, inv.y, oi.y);
+  const float r0z = fmaf(c.x, inv.z, oi.z), r1z = fmaf(c.w, inv.z, oi.z);
+  const float ln = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), kTMin));
+  const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), t.tbest));
+  const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kTMin));
+  const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), t.tbest));
+  // An empty slot (right child only; the host guarantees the left one is never empty) has an
+  // inverted box, which the symmetric min/max slab form would report as all of space: test
+  // the child code explicitly.
+  const bool hl = ln <= lf;
+  const bool hr = rn <= rf && ch.y != kEmptyChild;
+  if (hl && hr) {
+    const bool lfirst = ln <= rn;
+    if (t.sp < STACK) {
+      stk[t.sp * 64] = lfirst ? ch.y : ch.x;
+      ++t.sp;
+    } else {
+      overflow = true;
+    }
+    t.todo = lfirst ? ch.x : ch.y;
+  } else if (hl || hr) {
+    t.todo = hl ? ch.x : ch.y;
+  } else {
+    trav_pop(t, stk);
+  }
+}
+
+// Test the primitives of one leaf (t.todo < 0), then pop.
+template <bool COUNT>
+__device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
+                                          int32_t* stk, Counts<COUNT>& cnt, bool& corrupt) {
+  const int32_t code = ~t.todo;
+  const int32_t first = code >> 3;
+  const int32_t count = (code & 7) + 1;
+  if (static_cast<int64_t>(first) + count > S.num_refs) {
+    corrupt = true;
+    t.active = false;
+    return;
+  }
+  for (int k = 0; k < count; ++k) {
+    const int32_t ref = S.refs[first + k];
+    float th;
+    if (COUNT) cnt.prim += 1;
+    if (ref & kQuadRefBit) {
+      th = quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, t.tbest);
+    } else {
+      const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
+      th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest);
+    }
+    if (th > 0.0f) {  // th > tmin >= 0.001 on a hit
+      t.tbest = th;
+      t.best = ref;
+    }
+  }
+  trav_pop(t, stk);
+}
+
+// One unit of traversal work for this lane (used by the per-segment schedule).
+template <int STACK, bool COUNT>
+__device__ __forceinline__ void trav_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
+                                          int32_t* stk, Counts<COUNT>& cnt, bool& overflow,
+                                          bool& corrupt) {
+  if (t.todo >= 0)
+    node_step<STACK, COUNT>(t, S, stk, cnt, overflow, corrupt);
+  else
+    leaf_step<COUNT>(t, S, o, d, time, stk, cnt, corrupt);
+}
+
+// Schedule 2: the first kernel's monolithic closest-hit loop (kept for A/B).
 // Closest hit over the child-pair BVH (replaces hittable_list::hit -> bvh_node::hit ->
 // aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
 // traversal: the nearer child first, the farther pushed on the lane's LDS stack.
@@ -462,8 +582,246 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
+// Lane -> pixel mapping: a wave covers an 8x8 tile of the shard (rows are shard-local).
+struct LanePixel {
+  int i, lr, j;
+  uint32_t pixel_id;
+  bool valid;
+};
+__device__ __forceinline__ LanePixel tile_pixel(const DevCamera& C, const DevJob& J, int tx, int ty,
+                                                int lane) {
+  LanePixel p;
+  p.i = tx * 8 + (lane & 7);
+  p.lr = ty * 8 + (lane >> 3);
+  p.valid = p.i < C.width && p.lr < J.row_count;
+  p.j = J.row_begin + p.lr * J.row_stride;
+  p.pixel_id = static_cast<uint32_t>(p.j) * static_cast<uint32_t>(C.width) + static_cast<uint32_t>(p.i);
+  return p;
+}
+// non-persistent grids: a 256-thread workgroup covers 16x16 pixels (2x2 wave tiles)
+__device__ __forceinline__ LanePixel lane_pixel(const DevCamera& C, const DevJob& J, int lane, int wave) {
+  return tile_pixel(C, J, blockIdx.x * 2 + (wave & 1), blockIdx.y * 2 + (wave >> 1), lane);
+}
+
+// Per-wave accumulators that outlive one tile.
+template <bool COUNT>
+struct WaveStats {
+  uint32_t segs = 0, hits = 0;
+  Counts<COUNT> cnt;
+  bool overflow = false, corrupt = false;
+  uint64_t diag[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform schedule diagnostics (COUNT only)
+};
+
+template <bool COUNT>
+__device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w, int lane) {
+  const uint32_t wsegs = wave_sum(w.segs);
+  if (COUNT) {
+    const uint32_t wbox = wave_sum(w.cnt.box);
+    const uint32_t wprim = wave_sum(w.cnt.prim);
+    const uint32_t whits = wave_sum(w.hits);
+    if (lane == 0) {
+      atomicAdd(&J.counters[1], static_cast<unsigned long long>(wbox));
+      atomicAdd(&J.counters[2], static_cast<unsigned long long>(wprim));
+      atomicAdd(&J.counters[3], static_cast<unsigned long long>(whits));
+      for (int k = 0; k < 7; ++k) atomicAdd(&J.counters[8 + k], static_cast<unsigned long long>(w.diag[k]));
+    }
+  }
+  if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
+  if (__any(w.overflow) && lane == 0) atomicAdd(&J.counters[4], 1ull);
+  if (__any(w.corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
+}
+
+__device__ __forceinline__ void store_pixel(const DevCamera& C, const DevJob& J, const LanePixel& px, V3 acc) {
+  if (px.valid) {
+    float* o = J.out + (static_cast<int64_t>(px.lr) * C.width + px.i) * 3;
+    o[0] = C.scale * acc.x;
+    o[1] = C.scale * acc.y;
+    o[2] = C.scale * acc.z;
+  }
+}
+
+// One wave renders every sample of its 8x8 pixel tile with the ballot-batched schedule: every
+// lane advances its own traversal one step per trip; the wave switches to shading only once at
+// least ceil(alive * shade_batch / 64) lanes have finished their closest-hit query, so a wave no
+// longer waits for its slowest traversal before shading, and lanes still traversing keep their
+// stack and continue afterwards. Shaded lanes regenerate their path (next bounce or next sample
+// of the same pixel, in sample order) and re-enter traversal.
+template <int STACK, bool COUNT>
+__device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& C, const DevJob& J,
+                                            const LanePixel& px, int32_t* stk,
+                                            WaveStats<COUNT>& w) {
+  V3 acc = v3(0.0f, 0.0f, 0.0f);
+  int sample = 0;
+  bool done = !(px.valid && C.max_depth > 0 && C.spp > 0);
+  PathState ps;
+  Trav tr;
+  tr.active = false;
+  if (!done) {
+    start_sample(ps, C, J.seed_mix, px.pixel_id, 0, px.i, px.j);
+    trav_begin(tr, S, ps.o, ps.d);
+  }
+  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
+  for (;;) {
+    const int alive = __popcll(__ballot(!done));
+    if (alive == 0) break;
+    const int need = (alive * J.shade_batch + 63) >> 6;
+    uint64_t t_trav0 = 0;
+    if (COUNT) t_trav0 = __builtin_amdgcn_s_memtime();
+    for (;;) {
+      if (COUNT) {
+        w.diag[0] += 1;
+        w.diag[1] += __popcll(__ballot(tr.active));
+        w.diag[2] += __popcll(__ballot(done));
+      }
+      // A trip is either a node step or a leaf step for the whole wave, never both: leaf work
+      // (primitive tests) waits until leaf_batch lanes have reached a leaf or no lane has an
+      // inner node left, so the expensive primitive tests run with the lanes batched.
+      const int at_leaf = __popcll(__ballot(tr.active && tr.todo < 0));
+      const bool inner_left = __ballot(tr.active && tr.todo >= 0) != 0;
+      if (at_leaf >= J.leaf_batch || !inner_left) {
+        if (tr.active && tr.todo < 0) leaf_step<COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+      } else {
+        if (tr.active && tr.todo >= 0) node_step<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+      }
+      const uint64_t trav = __ballot(tr.active);
+      const int ready = __popcll(__ballot(!tr.active && !done));
+      if (trav == 0 || ready >= need) break;
+    }
+    uint64_t t_shade0 = 0;
+    if (COUNT) {
+      t_shade0 = __builtin_amdgcn_s_memtime();
+      w.diag[5] += t_shade0 - t_trav0;
+      w.diag[3] += 1;
+      w.diag[4] += __popcll(__ballot(!tr.active && !done));
+    }
+    if (!tr.active && !done) {
+      ++w.segs;
+      bool alive_path;
+      if (tr.best < 0) {
+        ps.L = add(ps.L, mul(ps.T, bg));
+        alive_path = false;
+      } else {
+        if (COUNT) ++w.hits;
+        alive_path = shade(S, ps, tr.best, tr.tbest);
+        if (alive_path && --ps.depth <= 0) alive_path = false;
+      }
+      if (!alive_path) {
+        acc = add(acc, ps.L);
+        ++sample;
+        if (sample < C.spp) {
+          start_sample(ps, C, J.seed_mix, px.pixel_id, sample, px.i, px.j);
+        } else {
+          done = true;
+        }
+      }
+      if (!done) trav_begin(tr, S, ps.o, ps.d);
+    }
+    if (COUNT) w.diag[6] += __builtin_amdgcn_s_memtime() - t_shade0;
+  }
+  store_pixel(C, J, px, acc);
+}
+
+// Schedule 0 on a plain grid (one wave = one 8x8 tile, 256-thread workgroups).
 template <int STACK, bool COUNT>
 __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
+  __shared__ int32_t s_stack[4 * STACK * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int32_t* stk = s_stack + wave * STACK * 64 + lane;
+  WaveStats<COUNT> w;
+  render_tile<STACK, COUNT>(S, C, J, lane_pixel(C, J, lane, wave), stk, w);
+  flush_stats<COUNT>(J, w, lane);
+}
+
+// Schedule 3 (default when the geometry fits): persistent workgroups of WAVES waves, one per CU.
+// The workgroup copies the traversal geometry (nodes, leaf refs, spheres, quads) into LDS once;
+// afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
+// L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
+// left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
+template <int STACK, bool COUNT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
+  float4* l_nodes = reinterpret_cast<float4*>(smem + J.lds_nodes);
+  int32_t* l_refs = reinterpret_cast<int32_t*>(smem + J.lds_refs);
+  float4* l_spheres = reinterpret_cast<float4*>(smem + J.lds_spheres);
+  float4* l_quads = reinterpret_cast<float4*>(smem + J.lds_quads);
+  for (int64_t k = threadIdx.x; k < S.num_nodes * 4; k += WAVES * 64) l_nodes[k] = S.nodes[k];
+  for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64) l_spheres[k] = S.spheres[k];
+  for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
+  for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
+  __syncthreads();
+  DevScene L = S;
+  L.nodes = l_nodes;
+  L.refs = l_refs;
+  L.spheres = l_spheres;
+  L.quads = l_quads;
+  WaveStats<COUNT> w;
+  for (;;) {
+    int tile = 0;
+    if (lane == 0) tile = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
+    tile = __shfl(tile, 0, 64);
+    if (tile >= J.num_tiles) break;
+    const int ty = tile / J.tiles_x;
+    const int tx = tile - ty * J.tiles_x;
+    render_tile<STACK, COUNT>(L, C, J, tile_pixel(C, J, tx, ty, lane), stk, w);
+  }
+  flush_stats<COUNT>(J, w, lane);
+}
+
+// Schedule 1: each loop trip runs one complete closest-hit query per lane through trav_step, so
+// the wave waits for its slowest traversal every segment.
+template <int STACK, bool COUNT>
+__global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCamera C, DevJob J) {
+  __shared__ int32_t s_stack[4 * STACK * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int32_t* stk = s_stack + wave * STACK * 64 + lane;
+  const LanePixel px = lane_pixel(C, J, lane, wave);
+
+  V3 acc = v3(0.0f, 0.0f, 0.0f);
+  uint32_t segs = 0, hits = 0;
+  Counts<COUNT> cnt;
+  bool overflow = false, corrupt = false;
+  int sample = (px.valid && C.max_depth > 0) ? 0 : C.spp;
+  PathState ps;
+  if (sample < C.spp) start_sample(ps, C, J.seed_mix, px.pixel_id, 0, px.i, px.j);
+  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
+  while (sample < C.spp) {
+    Trav tr;
+    trav_begin(tr, S, ps.o, ps.d);
+    while (tr.active) trav_step<STACK, COUNT>(tr, S, ps.o, ps.d, ps.time, stk, cnt, overflow, corrupt);
+    ++segs;
+    bool alive;
+    if (tr.best < 0) {
+      ps.L = add(ps.L, mul(ps.T, bg));
+      alive = false;
+    } else {
+      if (COUNT) ++hits;
+      alive = shade(S, ps, tr.best, tr.tbest);
+      if (alive && --ps.depth <= 0) alive = false;
+    }
+    if (!alive) {
+      acc = add(acc, ps.L);
+      ++sample;
+      if (sample < C.spp) start_sample(ps, C, J.seed_mix, px.pixel_id, sample, px.i, px.j);
+    }
+  }
+  store_pixel(C, J, px, acc);
+  WaveStats<COUNT> w;
+  w.segs = segs;
+  w.hits = hits;
+  w.cnt = cnt;
+  w.overflow = overflow;
+  w.corrupt = corrupt;
+  flush_stats<COUNT>(J, w, lane);
+}
+
+// Schedule 2: the first kernel (monolithic closest_hit loop), kept for A/B.
+template <int STACK, bool COUNT>
+__global__ __launch_bounds__(256) void render_kernel_v0(DevScene S, DevCamera C, DevJob J) {
   __shared__ int32_t s_stack[4 * STACK * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -536,15 +894,47 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
   out[k] = static_cast<uint8_t>(static_cast<int>(256.0f * x));
 }
 
+constexpr int kLdsWaves = 12;  // schedule 3: 768-thread persistent workgroups (<= 168 VGPRs)
+constexpr int kLdsWaves16 = 16;  // schedule 5: 1024-thread persistent workgroups (<= 128 VGPRs)
+
+template <int STACK, int WAVES>
+hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
+                      int lds_bytes, int grid_blocks, hipStream_t stream) {
+  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, true, WAVES>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, false, WAVES>);
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  if (e != hipSuccess) return e;
+  if (count)
+    hipLaunchKernelGGL((render_kernel_lds<STACK, true, WAVES>), dim3(grid_blocks), dim3(WAVES * 64),
+                       lds_bytes, stream, S, C, J);
+  else
+    hipLaunchKernelGGL((render_kernel_lds<STACK, false, WAVES>), dim3(grid_blocks), dim3(WAVES * 64),
+                       lds_bytes, stream, S, C, J);
+  return hipGetLastError();
+}
+
 template <int STACK>
 hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
-                        hipStream_t stream) {
+                        int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
+  if (variant == 3) return launch_lds<STACK, kLdsWaves>(S, C, J, count, lds_bytes, grid_blocks, stream);
+  if (variant == 5) return launch_lds<STACK, kLdsWaves16>(S, C, J, count, lds_bytes, grid_blocks, stream);
   const dim3 block(256);
   const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
-  if (count) {
-    hipLaunchKernelGGL((render_kernel<STACK, true>), grid, block, 0, stream, S, C, J);
+  if (variant == 2) {
+    if (count)
+      hipLaunchKernelGGL((render_kernel_v0<STACK, true>), grid, block, 0, stream, S, C, J);
+    else
+      hipLaunchKernelGGL((render_kernel_v0<STACK, false>), grid, block, 0, stream, S, C, J);
+  } else if (variant == 1) {
+    if (count)
+      hipLaunchKernelGGL((render_kernel_segment<STACK, true>), grid, block, 0, stream, S, C, J);
+    else
+      hipLaunchKernelGGL((render_kernel_segment<STACK, false>), grid, block, 0, stream, S, C, J);
   } else {
-    hipLaunchKernelGGL((render_kernel<STACK, false>), grid, block, 0, stream, S, C, J);
+    if (count)
+      hipLaunchKernelGGL((render_kernel<STACK, true>), grid, block, 0, stream, S, C, J);
+    else
+      hipLaunchKernelGGL((render_kernel<STACK, false>), grid, block, 0, stream, S, C, J);
   }
   return hipGetLastError();
 }
@@ -558,16 +948,39 @@ int kernel_stack_depth(int bvh_depth) {
   return -1;
 }
 
+// Dynamic LDS bytes of the persistent kernel for this scene, or -1 when it does not fit in
+// one CU's 160 KiB; fills the scene-copy offsets of the job.
+int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
+  auto a16 = [](int64_t x) { return (x + 15) & ~int64_t(15); };
+  int64_t off = int64_t(waves) * stack * 64 * 4;  // traversal stacks
+  const int64_t nodes = off;
+  off = a16(off + S.num_nodes * 64);
+  const int64_t spheres = off;
+  off = a16(off + S.num_spheres * 32);
+  const int64_t quads = off;
+  off = a16(off + S.num_quads * 80);
+  const int64_t refs = off;
+  off = a16(off + S.num_refs * 4);
+  if (off > 160 * 1024) return -1;
+  if (J) {
+    J->lds_nodes = static_cast<int32_t>(nodes);
+    J->lds_spheres = static_cast<int32_t>(spheres);
+    J->lds_quads = static_cast<int32_t>(quads);
+    J->lds_refs = static_cast<int32_t>(refs);
+  }
+  return static_cast<int>(off);
+}
+
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
-                         bool count, hipStream_t stream) {
+                         bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
   if (J.row_count <= 0 || C.width <= 0) return hipSuccess;
   switch (stack) {
     case 16:
-      return launch_stack<16>(S, C, J, count, stream);
+      return launch_stack<16>(S, C, J, count, variant, lds_bytes, grid_blocks, stream);
     case 32:
-      return launch_stack<32>(S, C, J, count, stream);
+      return launch_stack<32>(S, C, J, count, variant, lds_bytes, grid_blocks, stream);
     case 64:
-      return launch_stack<64>(S, C, J, count, stream);
+      return launch_stack<64>(S, C, J, count, variant, lds_bytes, grid_blocks, stream);
     default:
       return hipErrorInvalidValue;
   }

@@ -27,6 +27,18 @@ RTG_MAT_LAMBERTIAN, RTG_MAT_METAL, RTG_MAT_DIELECTRIC, RTG_MAT_DIFFUSE_LIGHT = 1
 RTG_TEX_SOLID, RTG_TEX_CHECKER, RTG_TEX_IMAGE, RTG_TEX_NOISE = 1, 2, 3, 4
 RTG_BVH_MEDIAN, RTG_BVH_SAH = 0, 1
 RTG_RENDER_OUT_DEVICE, RTG_RENDER_ASYNC, RTG_RENDER_COUNT = 0x1, 0x2, 0x4
+
+
+def RTG_RENDER_SCHEDULE(n: int) -> int:  # diagnostic kernel-schedule selector (include/rtgpu.h)
+    return (n & 0xFF) << 8
+
+
+def RTG_RENDER_SHADE_BATCH(n: int) -> int:
+    return (n & 0xFF) << 16
+
+
+def RTG_RENDER_LEAF_BATCH(n: int) -> int:
+    return (n & 0x7F) << 24
 DEFAULT_SEED = 0x5EED
 
 D3 = C.c_double * 3
@@ -86,7 +98,8 @@ class rtg_render_desc(C.Structure):
 
 class rtg_render_stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("box_tests", C.c_uint64),
-                ("prim_tests", C.c_uint64), ("hits", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("prim_tests", C.c_uint64), ("hits", C.c_uint64), ("kernel_ms", C.c_double),
+                ("diag", C.c_uint64 * 8)]
 
 
 class rtg_scene_info(C.Structure):

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""tools/diag.py — schedule diagnostics of the default kernel on one config (COUNT mode)."""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "raytracing-practice_amd", "python"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="bouncing_spheres")
+    ap.add_argument("--grid", type=int, default=11)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--batches", default="48")
+    a = ap.parse_args()
+    import rtgpu
+
+    lib = rtgpu.Library()
+    s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
+                                   spp=a.spp, max_depth=50)
+    ds = lib.scene_create(s.desc)
+    out = {}
+    for b in [int(x) for x in a.batches.split(",")]:
+        import ctypes as C
+        import numpy as np
+
+        H = lib.camera_resolve(s.camera).image_height
+        buf = np.zeros((H, a.width, 3), dtype=np.float32)
+        job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, rtgpu.RTG_RENDER_COUNT | (b << 16), None)
+        st = rtgpu.rtg_render_stats()
+        lib.check("rtg_render", lib.lib.rtg_render(ds.handle, C.byref(s.camera), C.byref(job),
+                                                    buf.ctypes.data, C.byref(st)))
+        d = list(st.diag)
+        out[b] = {"kernel_ms": round(st.kernel_ms, 1), "segments": st.segments,
+                  "trav_trips": d[0], "trav_lane_util": d[1] / (64 * d[0]),
+                  "idle_done_frac": d[2] / (64 * d[0]), "shade_trips": d[3],
+                  "shade_lane_util": d[4] / (64 * d[3]),
+                  "steps_per_segment": d[1] / st.segments,
+                  "box_tests_per_segment": st.box_tests / st.segments,
+                  "trav_cycles_frac": d[5] / max(1, d[5] + d[6]),
+                  "cycles_per_trav_trip": d[5] / max(1, d[0]),
+                  "cycles_per_shade_trip": d[6] / max(1, d[3])}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -12,6 +12,7 @@ import collections
 import csv
 import json
 import os
+import re
 import sys
 
 
@@ -31,7 +32,7 @@ def load(path, kernel_filter):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir", nargs="?", default="gpurun_out/prof")
-    ap.add_argument("--kernel", default="render_kernel<")
+    ap.add_argument("--kernel", default="render_kernel")
     ap.add_argument("--timed-only", action="store_true", default=True,
                     help="use the non-counting dispatches only")
     ap.add_argument("--workload", default=None)
@@ -45,7 +46,7 @@ def main():
         per, meta = load(p, a.kernel)
         for d, vals in per.items():
             name = meta[d][0]
-            if a.timed_only and ", true>" in name:
+            if a.timed_only and re.search(r"<\d+, true", name):
                 continue  # RTG_RENDER_COUNT variant
             for k, v in vals.items():
                 counters.setdefault(k, []).append(v)

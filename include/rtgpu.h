@@ -100,7 +100,7 @@ typedef struct rtg_perlin {
 
 /* BVH construction modes (the library always builds its own device BVH). */
 #define RTG_BVH_MEDIAN 0 /* bvh_node.hpp:25-77: longest axis, std::sort by bbox.min, median */
-#define RTG_BVH_SAH 1    /* binned SAH, leaves of <= 4 primitives */
+#define RTG_BVH_SAH 1    /* binned SAH, leaves of <= 4 primitives, collapsed to 4-wide nodes */
 
 typedef struct rtg_scene_desc {
   uint32_t abi_version; /* RTG_ABI_VERSION */
@@ -153,8 +153,8 @@ typedef struct rtg_camera_params {
 #define RTG_RENDER_COUNT 0x4      /* also count box / primitive tests (slower, diagnostic) */
 /* Diagnostic schedule selection (A/B of kernel variants; 0 = the default everywhere):
  * bits 8-15 schedule (0 default = 3 when the scene geometry fits in LDS else 4; 1 one closest-hit
- * query per loop trip; 2 the first kernel; 3 persistent LDS-resident geometry, 12 waves per
- * workgroup; 4 ballot-batched on a plain grid; 5 as 3 with 16 waves),
+ * query per loop trip; 2 the first kernel (1 and 2 need a binary BVH: RTG_BVH_MEDIAN); 3
+ * persistent 16-wave workgroups with LDS-resident geometry; 4 ballot-batched on a plain grid),
  * bits 16-23 shade batch of schedule 0 in 64ths of the live lanes (0 = library default). */
 #define RTG_RENDER_SCHEDULE(n) (((n) & 0xff) << 8)
 #define RTG_RENDER_SHADE_BATCH(n) (((n) & 0xff) << 16)
@@ -179,7 +179,8 @@ typedef struct rtg_render_stats {
   /* RTG_RENDER_COUNT only, wave-level schedule diagnostics (default schedule):
    * [0] traversal trips, [1] lanes stepping summed over trips, [2] lanes idle because their
    * pixel is finished summed over trips, [3] shading trips, [4] lanes shading summed over trips,
-   * [5] / [6] shader-clock cycles spent in the traversal / shading phases (s_memtime, all waves) */
+   * [5] / [6] shader-clock cycles spent in the traversal / shading phases (s_memtime, all waves),
+   * [7] traversal trips that were leaf trips */
   uint64_t diag[8];
 } rtg_render_stats;
 

@@ -26,8 +26,8 @@ using namespace rtg;
 
 namespace {
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
-constexpr int kDefaultLeafBatch = 16;   // lanes waiting at a leaf before a leaf trip
-constexpr int kDefaultLdsWaves = 12;    // persistent LDS workgroup size (schedule 3 = 12, 5 = 16)
+constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
+constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kNumCounters = 16;        // [0..6] see DevJob::counters, [8..14] diagnostics
 }
 
@@ -208,11 +208,25 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     }
   }
 
+  // internal mode 2 = SAH kept binary (diagnostic A/B of the node width)
+  rtg_scene_desc bd = *d;
+  const bool binary_sah = d->bvh_mode == 2;
+  if (binary_sah) bd.bvh_mode = RTG_BVH_SAH;
   Bvh bvh;
-  if (!build_bvh(d, &bvh, err)) return false;
+  if (!build_bvh(&bd, &bvh, err)) return false;
   out->num_prims = d->num_prims;
   out->num_nodes = static_cast<int64_t>(bvh.nodes.size());
   out->depth = bvh.depth;
+  out->stack_need = bvh.depth;
+  out->node_width = 2;
+  Bvh4 bvh4;
+  if (d->bvh_mode == RTG_BVH_SAH && !bvh.nodes.empty()) {
+    collapse_bvh4(bvh, &bvh4);
+    out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
+    out->depth = bvh4.depth;
+    out->stack_need = bvh4.max_pushes;
+    out->node_width = 4;
+  }
 
   // primitives, laid out in first-reference order for locality
   std::vector<int32_t> slot(d->num_prims, -1);
@@ -257,9 +271,46 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->refs[r] = (p.kind == RTG_PRIM_QUAD) ? (slot[pid] | kQuadRefBit) : slot[pid];
   }
 
-  // child-pair nodes: 64 B, boxes rounded outward, leaf = ~((first << 3) | (count - 1))
-  out->nodes.resize(bvh.nodes.size() * 16);
-  for (size_t k = 0; k < bvh.nodes.size(); ++k) {
+  // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
+  auto leaf_code = [&](int32_t child, int32_t count, int32_t* code) {
+    const int64_t first = -(static_cast<int64_t>(child) + 1);
+    if (count < 1 || count > 8 || first >= (int64_t(1) << 28)) {
+      *err = "BVH leaf not encodable";
+      return false;
+    }
+    *code = ~static_cast<int32_t>((first << 3) | (count - 1));
+    return true;
+  };
+  if (out->node_width == 4) {
+    // 4-wide nodes, 112 B: lo.x[4], lo.y[4], lo.z[4], hi.x[4], hi.y[4], hi.z[4], code[4]
+    out->nodes.resize(bvh4.nodes.size() * 28);
+    for (size_t k = 0; k < bvh4.nodes.size(); ++k) {
+      const BuildNode4& n = bvh4.nodes[k];
+      float* f = &out->nodes[k * 28];
+      if (n.child[0] == kEmptyChild) {
+        *err = "4-wide BVH node without children";
+        return false;
+      }
+      for (int c = 0; c < 4; ++c) {
+        int32_t code = kEmptyChild;
+        const bool empty = n.child[c] == kEmptyChild;
+        if (!empty) {
+          if (n.child[c] >= 0)
+            code = n.child[c];
+          else if (!leaf_code(n.child[c], n.count[c], &code))
+            return false;
+        }
+        for (int a = 0; a < 3; ++a) {
+          f[a * 4 + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
+          f[12 + a * 4 + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
+        }
+        f[24 + c] = ibits_to_float(code);
+      }
+    }
+  }
+  // child-pair nodes: 64 B
+  if (out->node_width == 2) out->nodes.resize(bvh.nodes.size() * 16);
+  for (size_t k = 0; out->node_width == 2 && k < bvh.nodes.size(); ++k) {
     const BuildNode& n = bvh.nodes[k];
     float lo[2][3], hi[2][3];
     int32_t code[2];
@@ -475,10 +526,10 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   HostScene hs;
   std::string err;
   if (!compile_scene(desc, &hs, &err)) return fail(RTG_E_INVALID, err);
-  const int stack = kernel_stack_depth(hs.depth);
+  const int stack = kernel_stack_depth(hs.stack_need);
   if (stack < 0)
-    return fail(RTG_E_UNSUPPORTED, "BVH depth " + std::to_string(hs.depth) +
-                                       " exceeds the deepest kernel stack (64)");
+    return fail(RTG_E_UNSUPPORTED, "BVH needs " + std::to_string(hs.stack_need) +
+                                       " stack entries, more than the deepest kernel stack (64)");
   const auto t1 = std::chrono::steady_clock::now();
 
   int ndev = 0;
@@ -560,6 +611,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
   s->dev.num_quads = static_cast<int64_t>(hs.quads.size() / 20);
+  s->dev.node_width = hs.node_width;
   s->num_cus = prop.multiProcessorCount;
 
   s->info.device = device;
@@ -675,12 +727,13 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dj.num_tiles = dj.tiles_x * ((rows + 7) / 8);
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
-  if (variant == 0) variant = lds_layout(s->dev, s->info.stack_depth, kDefaultLdsWaves, nullptr) > 0
-                                  ? (kDefaultLdsWaves == 16 ? 5 : 3) : 4;
-  const int lds_bytes = lds_layout(s->dev, s->info.stack_depth, variant == 5 ? 16 : 12, &dj);
+  const int lds_bytes = lds_layout(s->dev, s->info.stack_depth, kLdsWaves, &dj);
+  if (variant == 0) variant = lds_bytes > 0 ? 3 : 4;
+  if (variant == 5) variant = 3;  // former 16-wave alias
   if (variant == 4) variant = 0;  // plain-grid ballot schedule
-  if ((variant == 3 || variant == 5) && lds_bytes < 0)
-    return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
+  if (variant == 3 && lds_bytes < 0) return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
+  if ((variant == 1 || variant == 2) && s->dev.node_width != 2)
+    return fail(RTG_E_INVALID, "schedules 1 and 2 need a binary BVH (RTG_BVH_MEDIAN)");
   const int grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
   dj.counters = s->counters;
   RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");

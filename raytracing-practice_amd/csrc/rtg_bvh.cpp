@@ -289,6 +289,78 @@ void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]) {
   }
 }
 
+void collapse_bvh4(const Bvh& bin, Bvh4* out) {
+  out->nodes.clear();
+  out->depth = 0;
+  out->max_pushes = 0;
+  if (bin.nodes.empty()) return;
+  struct Slot {
+    int32_t code, count;
+    Box box;
+  };
+  auto slot_of = [&](const BuildNode& n, int side) {
+    Slot sl;
+    sl.code = n.child[side];
+    sl.count = n.count[side];
+    for (int k = 0; k < 3; ++k) {
+      sl.box.lo[k] = n.lo[side][k];
+      sl.box.hi[k] = n.hi[side][k];
+    }
+    return sl;
+  };
+  // recursive collapse; returns the new node index; tracks depth and stack pushes on the path
+  struct Rec {
+    const Bvh& bin;
+    Bvh4* out;
+    decltype(slot_of)& slot;
+    int32_t go(int32_t b, int depth, int pushes) {
+      out->depth = std::max(out->depth, depth);
+      std::vector<Slot> slots;
+      const BuildNode& n = bin.nodes[b];
+      for (int side = 0; side < 2; ++side)
+        if (n.child[side] != kEmptyChild) slots.push_back(slot(n, side));
+      while (slots.size() < 4) {
+        int best = -1;
+        double best_area = -1.0;
+        for (size_t i = 0; i < slots.size(); ++i) {
+          if (slots[i].code < 0) continue;
+          const double a = half_area(slots[i].box);
+          if (a > best_area) {
+            best_area = a;
+            best = static_cast<int>(i);
+          }
+        }
+        if (best < 0) break;
+        const BuildNode& c = bin.nodes[slots[best].code];
+        std::vector<Slot> kids;
+        for (int side = 0; side < 2; ++side)
+          if (c.child[side] != kEmptyChild) kids.push_back(slot(c, side));
+        if (kids.size() + slots.size() - 1 > 4) break;
+        slots.erase(slots.begin() + best);
+        slots.insert(slots.begin() + best, kids.begin(), kids.end());
+      }
+      const int32_t me = static_cast<int32_t>(out->nodes.size());
+      out->nodes.push_back(BuildNode4{});
+      const int here = pushes + static_cast<int>(slots.size()) - 1;
+      out->max_pushes = std::max(out->max_pushes, here);
+      int32_t codes[4] = {kEmptyChild, kEmptyChild, kEmptyChild, kEmptyChild};
+      for (size_t i = 0; i < slots.size(); ++i)
+        codes[i] = slots[i].code >= 0 ? go(slots[i].code, depth + 1, here) : slots[i].code;
+      BuildNode4& o = out->nodes[me];
+      for (int i = 0; i < 4; ++i) {
+        o.child[i] = codes[i];
+        o.count[i] = i < static_cast<int>(slots.size()) ? slots[i].count : 0;
+        for (int k = 0; k < 3; ++k) {
+          o.lo[i][k] = i < static_cast<int>(slots.size()) ? slots[i].box.lo[k] : kInf;
+          o.hi[i][k] = i < static_cast<int>(slots.size()) ? slots[i].box.hi[k] : -kInf;
+        }
+      }
+      return me;
+    }
+  } rec{bin, out, slot_of};
+  rec.go(0, 1, 0);
+}
+
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
   out->nodes.clear();
   out->refs.clear();

@@ -38,6 +38,8 @@ struct HostScene {
   std::vector<int32_t> perlin_perm;  // 3*256 per table
   int64_t num_nodes = 0;
   int32_t depth = 0;
+  int32_t stack_need = 0;  // traversal stack entries needed (<= depth for BVH2)
+  int32_t node_width = 2;  // 2: child-pair 64-B nodes, 4: 4-wide 128-B nodes
   int64_t num_prims = 0;
 };
 
@@ -54,6 +56,24 @@ struct Bvh {
   std::vector<int64_t> refs;  // primitive indices (into desc->prims)
   int32_t depth = 0;
 };
+
+// 4-wide node collapsed from the binary tree (2..4 children; unused slots kEmptyChild).
+struct BuildNode4 {
+  double lo[4][3];
+  double hi[4][3];
+  int32_t child[4];  // >= 0 node index, < 0 leaf -(1 + first ref), kEmptyChild unused
+  int32_t count[4];
+};
+
+struct Bvh4 {
+  std::vector<BuildNode4> nodes;
+  int32_t depth = 0;       // nodes on the longest root-to-leaf path
+  int32_t max_pushes = 0;  // most stack entries an ordered traversal can hold at once
+};
+
+// Collapse a binary child-pair BVH into a 4-wide one (greedy: open the largest-area inner child
+// until four slots are filled); leaf codes and refs are unchanged.
+void collapse_bvh4(const Bvh& bin, Bvh4* out);
 
 // aabb of one primitive exactly as the reference computes it (aabb.hpp:30-48,135-154;
 // sphere.hpp:16-44; quad.hpp:30-38).
@@ -95,6 +115,8 @@ struct DevScene {
   int64_t num_refs;
   int64_t num_spheres;
   int64_t num_quads;
+  int32_t node_width;  // 2 or 4 (see HostScene)
+  int32_t pad_;
 };
 
 struct DevJob {

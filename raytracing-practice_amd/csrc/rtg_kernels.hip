@@ -220,6 +220,71 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, int32_t* s
   }
 }
 
+__device__ __forceinline__ float slab_near(float ax, float ay, float az, float bx, float by, float bz,
+                                           V3 inv, V3 oi, float tbest) {
+  const float t0x = fmaf(ax, inv.x, oi.x), t1x = fmaf(bx, inv.x, oi.x);
+  const float t0y = fmaf(ay, inv.y, oi.y), t1y = fmaf(by, inv.y, oi.y);
+  const float t0z = fmaf(az, inv.z, oi.z), t1z = fmaf(bz, inv.z, oi.z);
+  const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), kTMin));
+  const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tbest));
+  return tn <= tf ? tn : __builtin_inff();
+}
+
+__device__ __forceinline__ void cswap(float& da, int32_t& ca, float& db, int32_t& cb) {
+  const bool sw = db < da;
+  const float d = sw ? db : da;
+  const int32_t c = sw ? cb : ca;
+  db = sw ? da : db;
+  cb = sw ? ca : cb;
+  da = d;
+  ca = c;
+}
+
+// Visit one 4-wide node: test the four child boxes (SoA: lo.x, lo.y, lo.z, hi.x, hi.y, hi.z,
+// codes), sort the hit children by entry distance with a 5-comparator network, continue with
+// the nearest and push the others far-to-near so the next nearest is popped first.
+template <int STACK, bool COUNT>
+__device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* stk, Counts<COUNT>& cnt,
+                                           bool& overflow, bool& corrupt) {
+  if (t.todo >= S.num_nodes) {
+    corrupt = true;
+    t.active = false;
+    return;
+  }
+  const float4* n = S.nodes + static_cast<int64_t>(t.todo) * 7;
+  const float4 lx = n[0], ly = n[1], lz = n[2], hx = n[3], hy = n[4], hz = n[5];
+  const int4 ch = *reinterpret_cast<const int4*>(n + 6);
+  if (COUNT) cnt.box += 4;
+  const V3 inv = t.inv, oi = t.oi;
+  // empty slots have inverted boxes, which the symmetric slab form would accept: mask by code
+  float d0 = slab_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, inv, oi, t.tbest);
+  float d1 = slab_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, inv, oi, t.tbest);
+  float d2 = slab_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, inv, oi, t.tbest);
+  float d3 = slab_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, inv, oi, t.tbest);
+  int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+  d1 = c1 == kEmptyChild ? __builtin_inff() : d1;
+  d2 = c2 == kEmptyChild ? __builtin_inff() : d2;
+  d3 = c3 == kEmptyChild ? __builtin_inff() : d3;
+  cswap(d0, c0, d1, c1);
+  cswap(d2, c2, d3, c3);
+  cswap(d0, c0, d2, c2);
+  cswap(d1, c1, d3, c3);
+  cswap(d1, c1, d2, c2);
+  if (d0 == __builtin_inff()) {
+    trav_pop(t, stk);
+    return;
+  }
+  const int npush = (d1 != __builtin_inff()) + (d2 != __builtin_inff()) + (d3 != __builtin_inff());
+  if (t.sp + npush > STACK) {
+    overflow = true;
+  } else {
+    if (d3 != __builtin_inff()) stk[(t.sp++) * 64] = c3;
+    if (d2 != __builtin_inff()) stk[(t.sp++) * 64] = c2;
+    if (d1 != __builtin_inff()) stk[(t.sp++) * 64] = c1;
+  }
+  t.todo = c0;
+}
+
 // Test the primitives of one leaf (t.todo < 0), then pop.
 template <bool COUNT>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
@@ -609,7 +674,7 @@ struct WaveStats {
   uint32_t segs = 0, hits = 0;
   Counts<COUNT> cnt;
   bool overflow = false, corrupt = false;
-  uint64_t diag[7] = {0, 0, 0, 0, 0, 0, 0};  // wave-uniform schedule diagnostics (COUNT only)
+  uint64_t diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform schedule diagnostics (COUNT only)
 };
 
 template <bool COUNT>
@@ -623,7 +688,7 @@ __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w
       atomicAdd(&J.counters[1], static_cast<unsigned long long>(wbox));
       atomicAdd(&J.counters[2], static_cast<unsigned long long>(wprim));
       atomicAdd(&J.counters[3], static_cast<unsigned long long>(whits));
-      for (int k = 0; k < 7; ++k) atomicAdd(&J.counters[8 + k], static_cast<unsigned long long>(w.diag[k]));
+      for (int k = 0; k < 8; ++k) atomicAdd(&J.counters[8 + k], static_cast<unsigned long long>(w.diag[k]));
     }
   }
   if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
@@ -646,7 +711,7 @@ __device__ __forceinline__ void store_pixel(const DevCamera& C, const DevJob& J,
 // longer waits for its slowest traversal before shading, and lanes still traversing keep their
 // stack and continue afterwards. Shaded lanes regenerate their path (next bounce or next sample
 // of the same pixel, in sample order) and re-enter traversal.
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, int WIDE>
 __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& C, const DevJob& J,
                                             const LanePixel& px, int32_t* stk,
                                             WaveStats<COUNT>& w) {
@@ -679,9 +744,15 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
       const int at_leaf = __popcll(__ballot(tr.active && tr.todo < 0));
       const bool inner_left = __ballot(tr.active && tr.todo >= 0) != 0;
       if (at_leaf >= J.leaf_batch || !inner_left) {
+        if (COUNT) w.diag[7] += 1;
         if (tr.active && tr.todo < 0) leaf_step<COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       } else {
-        if (tr.active && tr.todo >= 0) node_step<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+        if (tr.active && tr.todo >= 0) {
+          if constexpr (WIDE == 4)
+            node_step4<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+          else
+            node_step<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+        }
       }
       const uint64_t trav = __ballot(tr.active);
       const int ready = __popcll(__ballot(!tr.active && !done));
@@ -722,14 +793,14 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
 }
 
 // Schedule 0 on a plain grid (one wave = one 8x8 tile, 256-thread workgroups).
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, int WIDE>
 __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
   __shared__ int32_t s_stack[4 * STACK * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int32_t* stk = s_stack + wave * STACK * 64 + lane;
   WaveStats<COUNT> w;
-  render_tile<STACK, COUNT>(S, C, J, lane_pixel(C, J, lane, wave), stk, w);
+  render_tile<STACK, COUNT, WIDE>(S, C, J, lane_pixel(C, J, lane, wave), stk, w);
   flush_stats<COUNT>(J, w, lane);
 }
 
@@ -738,7 +809,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
 // L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
 // left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
-template <int STACK, bool COUNT, int WAVES>
+template <int STACK, bool COUNT, int WAVES, int WIDE>
 __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -748,7 +819,7 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   int32_t* l_refs = reinterpret_cast<int32_t*>(smem + J.lds_refs);
   float4* l_spheres = reinterpret_cast<float4*>(smem + J.lds_spheres);
   float4* l_quads = reinterpret_cast<float4*>(smem + J.lds_quads);
-  for (int64_t k = threadIdx.x; k < S.num_nodes * 4; k += WAVES * 64) l_nodes[k] = S.nodes[k];
+  for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) l_nodes[k] = S.nodes[k];
   for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64) l_spheres[k] = S.spheres[k];
   for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
   for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
@@ -766,7 +837,7 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
     if (tile >= J.num_tiles) break;
     const int ty = tile / J.tiles_x;
     const int tx = tile - ty * J.tiles_x;
-    render_tile<STACK, COUNT>(L, C, J, tile_pixel(C, J, tx, ty, lane), stk, w);
+    render_tile<STACK, COUNT, WIDE>(L, C, J, tile_pixel(C, J, tx, ty, lane), stk, w);
   }
   flush_stats<COUNT>(J, w, lane);
 }
@@ -894,30 +965,46 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
   out[k] = static_cast<uint8_t>(static_cast<int>(256.0f * x));
 }
 
-constexpr int kLdsWaves = 12;  // schedule 3: 768-thread persistent workgroups (<= 168 VGPRs)
-constexpr int kLdsWaves16 = 16;  // schedule 5: 1024-thread persistent workgroups (<= 128 VGPRs)
+constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
-template <int STACK, int WAVES>
+template <int STACK, int WIDE>
 hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                       int lds_bytes, int grid_blocks, hipStream_t stream) {
-  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, true, WAVES>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, false, WAVES>);
+  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, true, kLdsWaves, WIDE>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, false, kLdsWaves, WIDE>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (count)
-    hipLaunchKernelGGL((render_kernel_lds<STACK, true, WAVES>), dim3(grid_blocks), dim3(WAVES * 64),
-                       lds_bytes, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel_lds<STACK, true, kLdsWaves, WIDE>), dim3(grid_blocks),
+                       dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel_lds<STACK, false, WAVES>), dim3(grid_blocks), dim3(WAVES * 64),
-                       lds_bytes, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel_lds<STACK, false, kLdsWaves, WIDE>), dim3(grid_blocks),
+                       dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
+  return hipGetLastError();
+}
+
+template <int STACK, int WIDE>
+hipError_t launch_plain(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
+                        hipStream_t stream) {
+  const dim3 block(256);
+  const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
+  if (count)
+    hipLaunchKernelGGL((render_kernel<STACK, true, WIDE>), grid, block, 0, stream, S, C, J);
+  else
+    hipLaunchKernelGGL((render_kernel<STACK, false, WIDE>), grid, block, 0, stream, S, C, J);
   return hipGetLastError();
 }
 
 template <int STACK>
 hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                         int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
-  if (variant == 3) return launch_lds<STACK, kLdsWaves>(S, C, J, count, lds_bytes, grid_blocks, stream);
-  if (variant == 5) return launch_lds<STACK, kLdsWaves16>(S, C, J, count, lds_bytes, grid_blocks, stream);
+  const bool wide = S.node_width == 4;
+  if (variant == 3)
+    return wide ? launch_lds<STACK, 4>(S, C, J, count, lds_bytes, grid_blocks, stream)
+                : launch_lds<STACK, 2>(S, C, J, count, lds_bytes, grid_blocks, stream);
+  if (variant == 0)
+    return wide ? launch_plain<STACK, 4>(S, C, J, count, stream) : launch_plain<STACK, 2>(S, C, J, count, stream);
+  if (wide) return hipErrorInvalidValue;  // schedules 1 and 2 traverse binary nodes only
   const dim3 block(256);
   const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
   if (variant == 2) {
@@ -930,11 +1017,6 @@ hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, 
       hipLaunchKernelGGL((render_kernel_segment<STACK, true>), grid, block, 0, stream, S, C, J);
     else
       hipLaunchKernelGGL((render_kernel_segment<STACK, false>), grid, block, 0, stream, S, C, J);
-  } else {
-    if (count)
-      hipLaunchKernelGGL((render_kernel<STACK, true>), grid, block, 0, stream, S, C, J);
-    else
-      hipLaunchKernelGGL((render_kernel<STACK, false>), grid, block, 0, stream, S, C, J);
   }
   return hipGetLastError();
 }
@@ -954,7 +1036,7 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
   auto a16 = [](int64_t x) { return (x + 15) & ~int64_t(15); };
   int64_t off = int64_t(waves) * stack * 64 * 4;  // traversal stacks
   const int64_t nodes = off;
-  off = a16(off + S.num_nodes * 64);
+  off = a16(off + S.num_nodes * (S.node_width == 4 ? 112 : 64));
   const int64_t spheres = off;
   off = a16(off + S.num_spheres * 32);
   const int64_t quads = off;

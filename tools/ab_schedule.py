@@ -34,7 +34,7 @@ def main():
     import rtgpu
 
     lib = rtgpu.Library()
-    bvh = rtgpu.RTG_BVH_SAH if a.bvh == "sah" else rtgpu.RTG_BVH_MEDIAN
+    bvh = {"sah": rtgpu.RTG_BVH_SAH, "median": rtgpu.RTG_BVH_MEDIAN, "sah2": 2}[a.bvh]
     s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
                                    spp=a.spp, max_depth=50, bvh_mode=bvh)
     cam = s.camera

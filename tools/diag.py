@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--batches", default="48")
+    ap.add_argument("--leaf", type=int, default=0)
+    ap.add_argument("--schedule", type=int, default=0)
     a = ap.parse_args()
     import rtgpu
 
@@ -30,7 +32,8 @@ def main():
 
         H = lib.camera_resolve(s.camera).image_height
         buf = np.zeros((H, a.width, 3), dtype=np.float32)
-        job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, rtgpu.RTG_RENDER_COUNT | (b << 16), None)
+        job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, rtgpu.RTG_RENDER_COUNT | (b << 16) | (a.leaf << 24)
+                                    | (a.schedule << 8), None)
         st = rtgpu.rtg_render_stats()
         lib.check("rtg_render", lib.lib.rtg_render(ds.handle, C.byref(s.camera), C.byref(job),
                                                     buf.ctypes.data, C.byref(st)))
@@ -43,7 +46,8 @@ def main():
                   "box_tests_per_segment": st.box_tests / st.segments,
                   "trav_cycles_frac": d[5] / max(1, d[5] + d[6]),
                   "cycles_per_trav_trip": d[5] / max(1, d[0]),
-                  "cycles_per_shade_trip": d[6] / max(1, d[3])}
+                  "cycles_per_shade_trip": d[6] / max(1, d[3]),
+                  "leaf_trip_frac": d[7] / max(1, d[0])}
     print(json.dumps(out, indent=1))
 
 

@@ -612,6 +612,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
   s->dev.num_quads = static_cast<int64_t>(hs.quads.size() / 20);
   s->dev.node_width = hs.node_width;
+  s->dev.num_materials = static_cast<int32_t>(hs.materials.size() / 8);
+  s->dev.num_textures = static_cast<int32_t>(hs.textures.size() / 8);
   s->num_cus = prop.multiProcessorCount;
 
   s->info.device = device;

@@ -116,6 +116,8 @@ struct DevScene {
   int64_t num_spheres;
   int64_t num_quads;
   int32_t node_width;  // 2 or 4 (see HostScene)
+  int32_t num_materials;
+  int32_t num_textures;
   int32_t pad_;
 };
 
@@ -133,7 +135,7 @@ struct DevJob {
   int32_t tiles_x;    // 8x8 pixel tiles per shard row of tiles
   int32_t num_tiles;  // 8x8 pixel tiles in the shard
   // persistent LDS kernel: byte offsets of the scene copies in dynamic LDS
-  int32_t lds_nodes, lds_refs, lds_spheres, lds_quads;
+  int32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_materials, lds_textures;
 };
 
 }  // namespace rtg

@@ -819,6 +819,10 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   int32_t* l_refs = reinterpret_cast<int32_t*>(smem + J.lds_refs);
   float4* l_spheres = reinterpret_cast<float4*>(smem + J.lds_spheres);
   float4* l_quads = reinterpret_cast<float4*>(smem + J.lds_quads);
+  float4* l_materials = reinterpret_cast<float4*>(smem + J.lds_materials);
+  float4* l_textures = reinterpret_cast<float4*>(smem + J.lds_textures);
+  for (int k = threadIdx.x; k < S.num_materials * 2; k += WAVES * 64) l_materials[k] = S.materials[k];
+  for (int k = threadIdx.x; k < S.num_textures * 2; k += WAVES * 64) l_textures[k] = S.textures[k];
   for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) l_nodes[k] = S.nodes[k];
   for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64) l_spheres[k] = S.spheres[k];
   for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
@@ -829,6 +833,8 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   L.refs = l_refs;
   L.spheres = l_spheres;
   L.quads = l_quads;
+  L.materials = l_materials;
+  L.textures = l_textures;
   WaveStats<COUNT> w;
   for (;;) {
     int tile = 0;
@@ -1043,8 +1049,14 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
   off = a16(off + S.num_quads * 80);
   const int64_t refs = off;
   off = a16(off + S.num_refs * 4);
+  const int64_t materials = off;
+  off = a16(off + int64_t(S.num_materials) * 32);
+  const int64_t textures = off;
+  off = a16(off + int64_t(S.num_textures) * 32);
   if (off > 160 * 1024) return -1;
   if (J) {
+    J->lds_materials = static_cast<int32_t>(materials);
+    J->lds_textures = static_cast<int32_t>(textures);
     J->lds_nodes = static_cast<int32_t>(nodes);
     J->lds_spheres = static_cast<int32_t>(spheres);
     J->lds_quads = static_cast<int32_t>(quads);

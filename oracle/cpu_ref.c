@@ -682,7 +682,6 @@ static inline uint32_t pcg32(uint64_t* s) {
   return (xs >> rot) | (xs << ((32u - rot) & 31u));
 }
 static inline float U(uint64_t* s) { return (float)(pcg32(s) >> 8) * 5.9604644775390625e-8f; }
-static inline float U11(uint64_t* s) { return -1.0f + 2.0f * U(s); }
 
 /* exported for KATs */
 uint64_t orc_rng_state(uint64_t seed, uint32_t pixel, uint32_t sample) {
@@ -690,13 +689,51 @@ uint64_t orc_rng_state(uint64_t seed, uint32_t pixel, uint32_t sample) {
 }
 float orc_rng_uniform(uint64_t* state) { return U(state); }
 
+/* sin and cos of 2*pi*u, u in [0,1) (DESIGN.md rtg-f32 "direct sampling"): quadrant reduction and
+   Taylor polynomials on [-pi/4, pi/4), plain fp32 multiply/add only (no libm), so the GPU kernel
+   (rtg_kernels.hip sincos_turn) reproduces every bit. Used instead of the reference's rejection
+   loops (vec3.hpp:158-184), which make a wavefront wait for its unluckiest lane. */
+static void sincos_turn(float u, float* sn, float* cs) {
+  float t = 4.0f * u;
+  float q = floorf(t);
+  float x = (t - q - 0.5f) * 1.57079637f;
+  float x2 = x * x;
+  float sx = x + x * x2 * (-1.66666672e-1f + x2 * (8.33333377e-3f + x2 * (-1.98412701e-4f + x2 * 2.75573188e-6f)));
+  float cx = 1.0f + x2 * (-0.5f + x2 * (4.16666679e-2f + x2 * (-1.38888892e-3f +
+                                                              x2 * (2.48015876e-5f + x2 * -2.75573188e-7f))));
+  float a = (sx + cx) * 0.707106769f; /* sin(pi/4 + x) */
+  float b = (cx - sx) * 0.707106769f; /* cos(pi/4 + x) */
+  int qi = (int)q;
+  float c0 = (qi & 1) ? a : b, s0 = (qi & 1) ? b : a;
+  *cs = (qi == 1 || qi == 2) ? -c0 : c0;
+  *sn = (qi >= 2) ? -s0 : s0;
+}
+
+/* random_unit_vector (vec3.hpp:172-184), direct: z = 1 - 2U, then the azimuth from a second U */
 static f3 f32_random_unit_vector(uint64_t* s) {
-  for (int k = 0; k < 64; ++k) {
-    float x = U11(s), y = U11(s), z = U11(s);
-    float lensq = x * x + y * y + z * z;
-    if (0.0f < lensq && lensq <= 1.0f) return fscl(1.0f / sqrtf(lensq), F3(x, y, z));
-  }
-  return F3(1.0f, 0.0f, 0.0f);
+  float z = 1.0f - 2.0f * U(s);
+  float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float sn, cs;
+  sincos_turn(U(s), &sn, &cs);
+  return F3(r * cs, r * sn, z);
+}
+
+/* random_in_unit_disk (vec3.hpp:158-169), direct: radius sqrt(U), then the angle from a second U */
+static void f32_random_in_unit_disk(uint64_t* s, float* px, float* py) {
+  float r = sqrtf(U(s));
+  float sn, cs;
+  sincos_turn(U(s), &sn, &cs);
+  *px = r * cs;
+  *py = r * sn;
+}
+
+/* exported for the sampling checks (tests/test_oracle_parity.py) */
+void orc_sincos_turn(float u, float* sn, float* cs) { sincos_turn(u, sn, cs); }
+void orc_f32_unit_vector(uint64_t state, float out[3]) {
+  f3 v = f32_random_unit_vector(&state);
+  out[0] = v.x;
+  out[1] = v.y;
+  out[2] = v.z;
 }
 
 typedef struct {
@@ -924,15 +961,8 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
   f3 ps = fv_add(fv_add(p00, fscl((float)i + ox, du)), fscl((float)j + oy, dvv));
   f3 o = center;
   if (!(cam->defocus_angle <= 0.0f)) {
-    float px = 0.0f, py = 0.0f;
-    for (int k = 0; k < 64; ++k) {
-      float x = U11(&st), y = U11(&st);
-      if (x * x + y * y < 1.0f) {
-        px = x;
-        py = y;
-        break;
-      }
-    }
+    float px, py;
+    f32_random_in_unit_disk(&st, &px, &py);
     o = fv_add(fv_add(center, fscl(px, F3(cf[12], cf[13], cf[14]))), fscl(py, F3(cf[15], cf[16], cf[17])));
   }
   f3 d = fv_sub(ps, o);

@@ -283,6 +283,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   };
   if (out->node_width == 4) {
     // 4-wide nodes, 112 B: lo.x[4], lo.y[4], lo.z[4], hi.x[4], hi.y[4], hi.z[4], code[4]
+    if (bvh4.nodes.size() > static_cast<size_t>(INT32_MAX / 112)) {
+      *err = "BVH too large for 32-bit node offsets";
+      return false;
+    }
     out->nodes.resize(bvh4.nodes.size() * 28);
     for (size_t k = 0; k < bvh4.nodes.size(); ++k) {
       const BuildNode4& n = bvh4.nodes[k];
@@ -296,7 +300,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         const bool empty = n.child[c] == kEmptyChild;
         if (!empty) {
           if (n.child[c] >= 0)
-            code = n.child[c];
+            code = n.child[c] * 112;  // inner children: byte offset of the node
           else if (!leaf_code(n.child[c], n.count[c], &code))
             return false;
         }
@@ -614,6 +618,15 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.node_width = hs.node_width;
   s->dev.num_materials = static_cast<int32_t>(hs.materials.size() / 8);
   s->dev.num_textures = static_cast<int32_t>(hs.textures.size() / 8);
+  s->dev.ref_mode = 0;
+  {
+    bool ident_s = !hs.refs.empty(), ident_q = !hs.refs.empty();
+    for (size_t r = 0; r < hs.refs.size() && (ident_s || ident_q); ++r) {
+      ident_s = ident_s && hs.refs[r] == static_cast<int32_t>(r);
+      ident_q = ident_q && hs.refs[r] == (static_cast<int32_t>(r) | kQuadRefBit);
+    }
+    s->dev.ref_mode = ident_s ? 1 : (ident_q ? 2 : 0);
+  }
   s->num_cus = prop.multiProcessorCount;
 
   s->info.device = device;

@@ -11,6 +11,8 @@
 // RTG_BVH_SAH is this library's own binned-SAH builder (16 bins on centroids, leaves <= 4).
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <limits>
 
 #include "rtg_internal.hpp"
@@ -146,7 +148,8 @@ struct Builder {
 
   // ---- binned SAH ----
   static constexpr int kBins = 16;
-  static constexpr int kMaxLeaf = 4;
+  int kMaxLeaf = 4;        // primitives per leaf (<= 8, the leaf code's count field)
+  double trav_cost = 0.7;  // cost of one more level relative to one primitive test (measured best)
 
   // Returns a child code for the range; `node_depth` = depth of the node that would own it.
   int32_t sah_child(int64_t start, int64_t end, const Box& bbox, int depth, int32_t* count) {
@@ -207,7 +210,7 @@ struct Builder {
           best_split = b;
         }
       }
-      const double trav = 1.0 * half_area(bbox);
+      const double trav = trav_cost * half_area(bbox);
       if (n <= kMaxLeaf && leaf_cost <= best + trav) {
         *count = static_cast<int32_t>(n);
         return leaf(start, n);
@@ -378,6 +381,15 @@ bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
   out->nodes.reserve(n * 2);
   out->refs.reserve(n);
   Builder b{boxes, *out, ids};
+  // RTG_SAH_TUNE="trav_cost:max_leaf" overrides the SAH constants (tuning experiments only)
+  if (const char* tune = std::getenv("RTG_SAH_TUNE")) {
+    double ct = 0.0;
+    int ml = 0;
+    if (std::sscanf(tune, "%lf:%d", &ct, &ml) == 2 && ct > 0.0 && ml >= 1 && ml <= 8) {
+      b.trav_cost = ct;
+      b.kMaxLeaf = ml;
+    }
+  }
   if (desc->bvh_mode == RTG_BVH_MEDIAN) {
     b.median(0, n, 1);
   } else if (desc->bvh_mode == RTG_BVH_SAH) {

@@ -118,7 +118,9 @@ struct DevScene {
   int32_t node_width;  // 2 or 4 (see HostScene)
   int32_t num_materials;
   int32_t num_textures;
-  int32_t pad_;
+  // leaf reference mode: 0 = look up refs[]; 1 = refs[r] == r, all spheres; 2 = refs[r] == r | quad
+  // (single-kind scenes store primitives in reference order, so the indirection is the identity)
+  int32_t ref_mode;
 };
 
 struct DevJob {

@@ -28,7 +28,6 @@ namespace {
 
 constexpr float kTMin = 0.001f;  // interval(0.001, infinity), camera.hpp:192
 constexpr float kPi = 3.14159265358979323846f;
-constexpr int kMaxRejectTries = 64;
 constexpr int kMaxTexNesting = 16;
 
 struct V3 {
@@ -72,20 +71,35 @@ __device__ __forceinline__ uint32_t pcg_next(uint64_t& s) {
 __device__ __forceinline__ float uniform(uint64_t& s) {  // random_double(), [0,1), 24 bits
   return static_cast<float>(pcg_next(s) >> 8) * 5.9604644775390625e-8f;
 }
-__device__ __forceinline__ float uniform_m11(uint64_t& s) {  // random_double(-1, 1)
-  return -1.0f + 2.0f * uniform(s);
+
+// sin and cos of 2*pi*u, u in [0,1): quadrant reduction and Taylor polynomials on [-pi/4, pi/4),
+// plain fp32 multiply/add only, so oracle/cpu_ref.c (sincos_turn) reproduces every bit.
+__device__ __forceinline__ void sincos_turn(float u, float& sn, float& cs) {
+  const float t = 4.0f * u;
+  const float q = floorf(t);
+  const float x = (t - q - 0.5f) * 1.57079637f;
+  const float x2 = x * x;
+  const float sx =
+      x + x * x2 * (-1.66666672e-1f + x2 * (8.33333377e-3f + x2 * (-1.98412701e-4f + x2 * 2.75573188e-6f)));
+  const float cx = 1.0f + x2 * (-0.5f + x2 * (4.16666679e-2f + x2 * (-1.38888892e-3f +
+                                                                      x2 * (2.48015876e-5f + x2 * -2.75573188e-7f))));
+  const float a = (sx + cx) * 0.707106769f;  // sin(pi/4 + x)
+  const float b = (cx - sx) * 0.707106769f;  // cos(pi/4 + x)
+  const int qi = static_cast<int>(q);
+  const float c0 = (qi & 1) ? a : b, s0 = (qi & 1) ? b : a;
+  cs = (qi == 1 || qi == 2) ? -c0 : c0;
+  sn = (qi >= 2) ? -s0 : s0;
 }
 
-// random_unit_vector (vec3.hpp:172-184), draws x, y, z in that order.
+// random_unit_vector (vec3.hpp:172-184) by direct sampling (DESIGN.md rtg-f32): z = 1 - 2U, then
+// the azimuth from a second U. The reference's rejection loop would make every wave wait for its
+// unluckiest lane (~5 tries for 30 lanes at acceptance pi/6); this costs two draws, always.
 __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
-  for (int k = 0; k < kMaxRejectTries; ++k) {
-    const float x = uniform_m11(s);
-    const float y = uniform_m11(s);
-    const float z = uniform_m11(s);
-    const float lensq = x * x + y * y + z * z;
-    if (0.0f < lensq && lensq <= 1.0f) return scl(1.0f / sqrtf(lensq), v3(x, y, z));
-  }
-  return v3(1.0f, 0.0f, 0.0f);
+  const float z = 1.0f - 2.0f * uniform(s);
+  const float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float sn, cs;
+  sincos_turn(uniform(s), sn, cs);
+  return v3(r * cs, r * sn, z);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -149,14 +163,19 @@ struct Trav {
   V3 inv, oi;     // 1/d and -o/d for the fused slab test
   float tbest;    // closest hit so far (the shrinking interval.max of the reference)
   int32_t best;   // primitive ref of the closest hit, -1 = none
-  int32_t todo;   // node index (>= 0) or leaf code (< 0) to visit next
+  int32_t todo;   // inner node (>= 0: index, or byte offset in 4-wide trees) or leaf code (< 0)
   int32_t sp;     // stack depth
+  int32_t sx, sy, sz;  // 4-wide nodes: 48 where the direction component is negative, else 0
   bool active;    // traversal not finished
 };
 
 __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d) {
   t.inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
   t.oi = v3(-o.x * t.inv.x, -o.y * t.inv.y, -o.z * t.inv.z);
+  // near slab plane per axis: lo (SoA row a) when 1/d >= 0, hi (row a + 3, 48 B further) when < 0
+  t.sx = (static_cast<uint32_t>(ibits(t.inv.x)) >> 31) * 48;
+  t.sy = (static_cast<uint32_t>(ibits(t.inv.y)) >> 31) * 48;
+  t.sz = (static_cast<uint32_t>(ibits(t.inv.z)) >> 31) * 48;
   t.tbest = __builtin_inff();
   t.best = -1;
   t.todo = 0;
@@ -220,69 +239,82 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, int32_t* s
   }
 }
 
-__device__ __forceinline__ float slab_near(float ax, float ay, float az, float bx, float by, float bz,
-                                           V3 inv, V3 oi, float tbest) {
-  const float t0x = fmaf(ax, inv.x, oi.x), t1x = fmaf(bx, inv.x, oi.x);
-  const float t0y = fmaf(ay, inv.y, oi.y), t1y = fmaf(by, inv.y, oi.y);
-  const float t0z = fmaf(az, inv.z, oi.z), t1z = fmaf(bz, inv.z, oi.z);
-  const float tn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), kTMin));
-  const float tf = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), tbest));
-  return tn <= tf ? tn : __builtin_inff();
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Entry distance of one child (tn) or a miss: the slab test with the near/far planes already
+// chosen by the ray's direction signs, so no min/max between a slab's two planes is needed.
+__device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, float tfx, float tfy,
+                                              float tfz, float tbest, uint32_t slot) {
+  const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kTMin);
+  const float tf = fminf(fminf(fminf(tfx, tfy), tfz), tbest);
+  // tn >= kTMin > 0, so its bits order like the float; the low 4 bits carry the slot (x4)
+  return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
 
-__device__ __forceinline__ void cswap(float& da, int32_t& ca, float& db, int32_t& cb) {
-  const bool sw = db < da;
-  const float d = sw ? db : da;
-  const int32_t c = sw ? cb : ca;
-  db = sw ? da : db;
-  cb = sw ? ca : cb;
-  da = d;
-  ca = c;
+__device__ __forceinline__ void usort(uint32_t& a, uint32_t& b) {
+  const uint32_t lo = min(a, b);
+  b = max(a, b);
+  a = lo;
 }
 
-// Visit one 4-wide node: test the four child boxes (SoA: lo.x, lo.y, lo.z, hi.x, hi.y, hi.z,
-// codes), sort the hit children by entry distance with a 5-comparator network, continue with
-// the nearest and push the others far-to-near so the next nearest is popped first.
+// Visit one 4-wide node (SoA rows lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, code; 16 B each). Per ray
+// the near plane of each axis is fixed by the sign of 1/d (Trav::sx/sy/sz pick the row), so each
+// child costs 6 fma (packed two children per v_pk_fma_f32) + max3/max + min3/min. The four hit
+// children are sorted as integer keys (entry distance with the slot in the low bits) by a
+// 5-comparator min/max network; the nearest becomes the next node, the others are pushed
+// far-to-near. Empty slots hold the inverted box (+inf, -inf): whatever the signs, at least one
+// axis has a finite 1/d, for which the near plane gives tn = +inf and the far one tf = -inf, so an
+// empty slot can never be entered (rays with all three components zero do not exist).
 template <int STACK, bool COUNT>
 __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
-  if (t.todo >= S.num_nodes) {
+  // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
+  if (t.todo >= S.num_nodes * 112) {
     corrupt = true;
     t.active = false;
     return;
   }
-  const float4* n = S.nodes + static_cast<int64_t>(t.todo) * 7;
-  const float4 lx = n[0], ly = n[1], lz = n[2], hx = n[3], hy = n[4], hz = n[5];
-  const int4 ch = *reinterpret_cast<const int4*>(n + 6);
+  const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
+  const float4 nx = *reinterpret_cast<const float4*>(nb + t.sx);
+  const float4 ny = *reinterpret_cast<const float4*>(nb + 16 + t.sy);
+  const float4 nz = *reinterpret_cast<const float4*>(nb + 32 + t.sz);
+  const float4 fx = *reinterpret_cast<const float4*>(nb + 48 - t.sx);
+  const float4 fy = *reinterpret_cast<const float4*>(nb + 64 - t.sy);
+  const float4 fz = *reinterpret_cast<const float4*>(nb + 80 - t.sz);
   if (COUNT) cnt.box += 4;
-  const V3 inv = t.inv, oi = t.oi;
-  // empty slots have inverted boxes, which the symmetric slab form would accept: mask by code
-  float d0 = slab_near(lx.x, ly.x, lz.x, hx.x, hy.x, hz.x, inv, oi, t.tbest);
-  float d1 = slab_near(lx.y, ly.y, lz.y, hx.y, hy.y, hz.y, inv, oi, t.tbest);
-  float d2 = slab_near(lx.z, ly.z, lz.z, hx.z, hy.z, hz.z, inv, oi, t.tbest);
-  float d3 = slab_near(lx.w, ly.w, lz.w, hx.w, hy.w, hz.w, inv, oi, t.tbest);
-  int32_t c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-  d1 = c1 == kEmptyChild ? __builtin_inff() : d1;
-  d2 = c2 == kEmptyChild ? __builtin_inff() : d2;
-  d3 = c3 == kEmptyChild ? __builtin_inff() : d3;
-  cswap(d0, c0, d1, c1);
-  cswap(d2, c2, d3, c3);
-  cswap(d0, c0, d2, c2);
-  cswap(d1, c1, d3, c3);
-  cswap(d1, c1, d2, c2);
-  if (d0 == __builtin_inff()) {
+  const f2 ix = {t.inv.x, t.inv.x}, iy = {t.inv.y, t.inv.y}, iz = {t.inv.z, t.inv.z};
+  const f2 ox = {t.oi.x, t.oi.x}, oy = {t.oi.y, t.oi.y}, oz = {t.oi.z, t.oi.z};
+  const f2 nx01 = pk_fma(f2{nx.x, nx.y}, ix, ox), nx23 = pk_fma(f2{nx.z, nx.w}, ix, ox);
+  const f2 ny01 = pk_fma(f2{ny.x, ny.y}, iy, oy), ny23 = pk_fma(f2{ny.z, ny.w}, iy, oy);
+  const f2 nz01 = pk_fma(f2{nz.x, nz.y}, iz, oz), nz23 = pk_fma(f2{nz.z, nz.w}, iz, oz);
+  const f2 fx01 = pk_fma(f2{fx.x, fx.y}, ix, ox), fx23 = pk_fma(f2{fx.z, fx.w}, ix, ox);
+  const f2 fy01 = pk_fma(f2{fy.x, fy.y}, iy, oy), fy23 = pk_fma(f2{fy.z, fy.w}, iy, oy);
+  const f2 fz01 = pk_fma(f2{fz.x, fz.y}, iz, oz), fz23 = pk_fma(f2{fz.z, fz.w}, iz, oz);
+  uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, t.tbest, 0);
+  uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, t.tbest, 4);
+  uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, t.tbest, 8);
+  uint32_t k3 = child_key(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, t.tbest, 12);
+  usort(k0, k1);
+  usort(k2, k3);
+  usort(k0, k2);
+  usort(k1, k3);
+  usort(k1, k2);
+  if (k0 == ~0u) {
     trav_pop(t, stk);
     return;
   }
-  const int npush = (d1 != __builtin_inff()) + (d2 != __builtin_inff()) + (d3 != __builtin_inff());
+  const char* codes = nb + 96;
+  auto code_of = [&](uint32_t k) { return *reinterpret_cast<const int32_t*>(codes + (k & 12u)); };
+  const int npush = (k1 != ~0u) + (k2 != ~0u) + (k3 != ~0u);
   if (t.sp + npush > STACK) {
     overflow = true;
   } else {
-    if (d3 != __builtin_inff()) stk[(t.sp++) * 64] = c3;
-    if (d2 != __builtin_inff()) stk[(t.sp++) * 64] = c2;
-    if (d1 != __builtin_inff()) stk[(t.sp++) * 64] = c1;
+    if (k3 != ~0u) stk[(t.sp++) * 64] = code_of(k3);
+    if (k2 != ~0u) stk[(t.sp++) * 64] = code_of(k2);
+    if (k1 != ~0u) stk[(t.sp++) * 64] = code_of(k1);
   }
-  t.todo = c0;
+  t.todo = code_of(k0);
 }
 
 // Test the primitives of one leaf (t.todo < 0), then pop.
@@ -297,8 +329,21 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     t.active = false;
     return;
   }
+  if (S.ref_mode == 1) {  // sphere-only scene, primitives stored in reference order
+    for (int k = 0; k < count; ++k) {
+      const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * 2;
+      if (COUNT) cnt.prim += 1;
+      const float th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest);
+      if (th > 0.0f) {
+        t.tbest = th;
+        t.best = first + k;
+      }
+    }
+    trav_pop(t, stk);
+    return;
+  }
   for (int k = 0; k < count; ++k) {
-    const int32_t ref = S.refs[first + k];
+    const int32_t ref = S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit);
     float th;
     if (COUNT) cnt.prim += 1;
     if (ref & kQuadRefBit) {
@@ -524,16 +569,11 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
   const V3 sample_pt = add(add(p00, scl(fi, du)), scl(fj, dv));
   V3 origin = v3(C.center[0], C.center[1], C.center[2]);
   if (C.defocus) {
-    float px = 0.0f, py = 0.0f;
-    for (int k = 0; k < kMaxRejectTries; ++k) {
-      const float x = uniform_m11(ps.rng);
-      const float y = uniform_m11(ps.rng);
-      if (x * x + y * y < 1.0f) {
-        px = x;
-        py = y;
-        break;
-      }
-    }
+    // random_in_unit_disk (vec3.hpp:158-169), direct: radius sqrt(U), angle from a second U
+    const float r = sqrtf(uniform(ps.rng));
+    float sn, cs;
+    sincos_turn(uniform(ps.rng), sn, cs);
+    const float px = r * cs, py = r * sn;
     origin = add(add(origin, scl(px, v3(C.defu[0], C.defu[1], C.defu[2]))),
                  scl(py, v3(C.defv[0], C.defv[1], C.defv[2])));
   }
@@ -593,21 +633,23 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
     return false;
   }
   V3 dir, att;
-  if (type == RTG_MAT_LAMBERTIAN) {
+  if (type == RTG_MAT_LAMBERTIAN || type == RTG_MAT_METAL) {
+    // both scatter around a random unit vector: one sampling code path for the lanes of either
     const V3 r = random_unit_vector(ps.rng);
-    dir = add(n, r);
-    // near_zero with the reference's fabs(e[1] < s) quirk (vec3.hpp:70-77, H5)
-    const float s = 1e-8f;
-    if (fabsf(dir.x) < s && dir.y < s && fabsf(dir.z) < s) dir = n;
-    if (needs_uv) sphere_uv();
-    att = texture_value(S, tex, u, v, p);
-  } else if (type == RTG_MAT_METAL) {
-    const V3 in = ps.d;
-    const V3 refl = sub(in, scl(2.0f * dot(in, n), n));
-    const V3 r = random_unit_vector(ps.rng);
-    dir = add(unit(refl), scl(m0.z, r));
-    att = xyz(m1);
-    if (!(dot(dir, n) > 0.0f)) return false;  // absorbed: color_from_emission == 0
+    if (type == RTG_MAT_LAMBERTIAN) {
+      dir = add(n, r);
+      // near_zero with the reference's fabs(e[1] < s) quirk (vec3.hpp:70-77, H5)
+      const float s = 1e-8f;
+      if (fabsf(dir.x) < s && dir.y < s && fabsf(dir.z) < s) dir = n;
+      if (needs_uv) sphere_uv();
+      att = texture_value(S, tex, u, v, p);
+    } else {
+      const V3 in = ps.d;
+      const V3 refl = sub(in, scl(2.0f * dot(in, n), n));
+      dir = add(unit(refl), scl(m0.z, r));
+      att = xyz(m1);
+      if (!(dot(dir, n) > 0.0f)) return false;  // absorbed: color_from_emission == 0
+    }
   } else if (type == RTG_MAT_DIELECTRIC) {
     att = v3(1.0f, 1.0f, 1.0f);
     const float eta = m0.w;
@@ -826,7 +868,8 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) l_nodes[k] = S.nodes[k];
   for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64) l_spheres[k] = S.spheres[k];
   for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
-  for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
+  if (S.ref_mode == 0)
+    for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
@@ -1048,7 +1091,7 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
   const int64_t quads = off;
   off = a16(off + S.num_quads * 80);
   const int64_t refs = off;
-  off = a16(off + S.num_refs * 4);
+  off = a16(off + (S.ref_mode == 0 ? S.num_refs * 4 : 0));
   const int64_t materials = off;
   off = a16(off + int64_t(S.num_materials) * 32);
   const int64_t textures = off;

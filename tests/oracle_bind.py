@@ -47,6 +47,18 @@ class Oracle:
         L.orc_bvh_replay.argtypes = [P(rtgpu.rtg_scene_desc), D3P, D3P, C.c_double, P(C.c_int64),
                                      C.c_int64, D3P]
         L.orc_bvh_replay.restype = C.c_int64
+        L.orc_sincos_turn.argtypes = [C.c_float, P(C.c_float), P(C.c_float)]
+        L.orc_f32_unit_vector.argtypes = [C.c_uint64, P(C.c_float)]
+
+    def sincos_turn(self, u):
+        sn, cs = C.c_float(), C.c_float()
+        self.lib.orc_sincos_turn(u, C.byref(sn), C.byref(cs))
+        return sn.value, cs.value
+
+    def unit_vector(self, state):
+        out = (C.c_float * 3)()
+        self.lib.orc_f32_unit_vector(state, out)
+        return tuple(out)
 
     @staticmethod
     def _d(v):

@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
-"""tools/ab_schedule.py — interleaved in-process A/B of render-kernel schedules on one device.
+"""tools/ab_schedule.py — interleaved in-process A/B of render kernels on one device.
 
   python3 tools/ab_schedule.py [--rounds 3] [--variants 0:48,0:32,1:0] [--spp 500]
+                               [--libs new=raytracing-practice_amd/lib/librtgpu.so,base=...]
 
 Each variant "S:B:L" = schedule S (include/rtgpu.h RTG_RENDER_SCHEDULE) with shade batch B (64ths)
-and leaf batch L (lanes); 0 = library default. Renders BASELINE config 2 (book-1, 1920x1080, depth 50) and reports the
-kernel time (HIP events) per variant per round plus the median Mrays/s; checks that every
-variant produced the identical frame.
+and leaf batch L (lanes); 0 = library default. A variant may be prefixed "name@" to pick one of
+the --libs builds (default: the first) and suffixed "#ct:ml" to build its BVH with SAH traversal
+cost ct and max leaf size ml (RTG_SAH_TUNE). Renders BASELINE config 2 (book-1, 1920x1080, depth 50)
+and reports the kernel time (HIP events) per variant per round plus the median Mrays/s; checks
+every variant's frame against the first one (identical, or the fraction of equal pixels).
 """
 import argparse
 import json
@@ -22,38 +25,62 @@ sys.path.insert(0, os.path.join(REPO, "raytracing-practice_amd", "python"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="0:48,0:32,0:56,0:64,1:0")
+    ap.add_argument("--variants", default="0:0:0")
+    ap.add_argument("--libs", default="")
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--grid", type=int, default=11)
     ap.add_argument("--scene", default="bouncing_spheres")
     ap.add_argument("--bvh", default="sah")
+    ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()
     import torch
 
     import rtgpu
 
-    lib = rtgpu.Library()
+    libs = {}
+    for item in filter(None, a.libs.split(",")):
+        name, path = item.split("=", 1)
+        libs[name] = rtgpu.Library(os.path.join(REPO, path) if not os.path.isabs(path) else path)
+    if not libs:
+        libs["lib"] = rtgpu.Library()
+    first = next(iter(libs))
     bvh = {"sah": rtgpu.RTG_BVH_SAH, "median": rtgpu.RTG_BVH_MEDIAN, "sah2": 2}[a.bvh]
     s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
-                                   spp=a.spp, max_depth=50, bvh_mode=bvh)
+                                   spp=a.spp, max_depth=a.depth, bvh_mode=bvh)
     cam = s.camera
-    H = lib.camera_resolve(cam).image_height
-    ds = lib.scene_create(s.desc)
+    H = libs[first].camera_resolve(cam).image_height
+    scenes = {}
+
+    def scene_for(name, tune):
+        if (name, tune) not in scenes:
+            if tune:
+                os.environ["RTG_SAH_TUNE"] = tune
+            else:
+                os.environ.pop("RTG_SAH_TUNE", None)
+            scenes[(name, tune)] = libs[name].scene_create(s.desc)
+            os.environ.pop("RTG_SAH_TUNE", None)
+        return scenes[(name, tune)]
     out = torch.zeros((H, a.width, 3), device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
-    variants = [tuple(int(x) for x in (v.split(":") + ["0", "0"])[:3]) for v in a.variants.split(",")]
+
+    variants = []
+    for v in a.variants.split(","):
+        name, spec = (v.split("@", 1) if "@" in v else (first, v))
+        spec, tune = (spec.split("#", 1) if "#" in spec else (spec, ""))
+        nums = tuple(int(x) for x in (spec.split(":") + ["0", "0"])[:3])
+        variants.append((name, nums, tune))
     times = {v: [] for v in variants}
-    frames = {}
-    segs = {}
+    frames, segs = {}, {}
     for r in range(a.rounds):
         for v in variants:
-            sched, batch, leaf = v
+            name, (sched, batch, leaf), tune = v
+            L, ds = libs[name], scene_for(name, tune)
             flags = rtgpu.RTG_RENDER_OUT_DEVICE | (sched << 8) | (batch << 16) | (leaf << 24)
             job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, flags, stream)
             st = rtgpu.rtg_render_stats()
-            lib.check("rtg_render", lib.lib.rtg_render(ds.handle, rtgpu.C.byref(cam), rtgpu.C.byref(job),
-                                                        out.data_ptr(), rtgpu.C.byref(st)))
+            L.check("rtg_render", L.lib.rtg_render(ds.handle, rtgpu.C.byref(cam), rtgpu.C.byref(job),
+                                                    out.data_ptr(), rtgpu.C.byref(st)))
             times[v].append(st.kernel_ms)
             segs[v] = st.segments
             if r == 0:
@@ -62,11 +89,15 @@ def main():
     res = {}
     for v in variants:
         med = float(np.median(times[v]))
-        res[":".join(str(x) for x in v)] = {"kernel_ms": [round(t, 2) for t in times[v]], "median_ms": round(med, 2),
-                                 "mrays_per_s": round(segs[v] / med / 1e3, 1),
-                                 "identical_frame": bool(np.array_equal(frames[v], base))}
-    print(json.dumps({"scene": a.scene, "grid": a.grid, "spp": a.spp, "width": a.width, "results": res},
-                     indent=1))
+        key = f"{v[0]}@" + ":".join(str(x) for x in v[1]) + (f"#{v[2]}" if v[2] else "")
+        res[key] = {"kernel_ms": [round(t, 2) for t in times[v]], "median_ms": round(med, 2),
+                    "mrays_per_s": round(segs[v] / med / 1e3, 1), "segments": int(segs[v]),
+                    "identical_frame": bool(np.array_equal(frames[v], base)),
+                    "equal_pixel_frac": float(np.mean(np.all(frames[v] == base, axis=-1)))}
+    for ds in scenes.values():
+        ds.close()
+    print(json.dumps({"scene": a.scene, "grid": a.grid, "spp": a.spp, "width": a.width, "depth": a.depth,
+                      "results": res}, indent=1))
 
 
 if __name__ == "__main__":

@@ -627,6 +627,10 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     }
     s->dev.ref_mode = ident_s ? 1 : (ident_q ? 2 : 0);
   }
+  s->dev.tex_full = 0;
+  for (int32_t t = 0; t < desc->num_textures; ++t)
+    if (desc->textures[t].type == RTG_TEX_IMAGE || desc->textures[t].type == RTG_TEX_NOISE) s->dev.tex_full = 1;
+  s->dev.pad_ = 0;
   s->num_cus = prop.multiProcessorCount;
 
   s->info.device = device;

@@ -121,6 +121,8 @@ struct DevScene {
   // leaf reference mode: 0 = look up refs[]; 1 = refs[r] == r, all spheres; 2 = refs[r] == r | quad
   // (single-kind scenes store primitives in reference order, so the indirection is the identity)
   int32_t ref_mode;
+  int32_t tex_full;  // 1 when some texture is an image or noise texture (kernel variant selector)
+  int32_t pad_;
 };
 
 struct DevJob {

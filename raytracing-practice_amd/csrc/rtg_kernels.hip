@@ -165,17 +165,12 @@ struct Trav {
   int32_t best;   // primitive ref of the closest hit, -1 = none
   int32_t todo;   // inner node (>= 0: index, or byte offset in 4-wide trees) or leaf code (< 0)
   int32_t sp;     // stack depth
-  int32_t sx, sy, sz;  // 4-wide nodes: 48 where the direction component is negative, else 0
   bool active;    // traversal not finished
 };
 
 __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d) {
   t.inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
   t.oi = v3(-o.x * t.inv.x, -o.y * t.inv.y, -o.z * t.inv.z);
-  // near slab plane per axis: lo (SoA row a) when 1/d >= 0, hi (row a + 3, 48 B further) when < 0
-  t.sx = (static_cast<uint32_t>(ibits(t.inv.x)) >> 31) * 48;
-  t.sy = (static_cast<uint32_t>(ibits(t.inv.y)) >> 31) * 48;
-  t.sz = (static_cast<uint32_t>(ibits(t.inv.z)) >> 31) * 48;
   t.tbest = __builtin_inff();
   t.best = -1;
   t.todo = 0;
@@ -276,12 +271,15 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* 
     return;
   }
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
-  const float4 nx = *reinterpret_cast<const float4*>(nb + t.sx);
-  const float4 ny = *reinterpret_cast<const float4*>(nb + 16 + t.sy);
-  const float4 nz = *reinterpret_cast<const float4*>(nb + 32 + t.sz);
-  const float4 fx = *reinterpret_cast<const float4*>(nb + 48 - t.sx);
-  const float4 fy = *reinterpret_cast<const float4*>(nb + 64 - t.sy);
-  const float4 fz = *reinterpret_cast<const float4*>(nb + 80 - t.sz);
+  const int32_t sx = (static_cast<uint32_t>(ibits(t.inv.x)) >> 31) * 48;
+  const int32_t sy = (static_cast<uint32_t>(ibits(t.inv.y)) >> 31) * 48;
+  const int32_t sz = (static_cast<uint32_t>(ibits(t.inv.z)) >> 31) * 48;
+  const float4 nx = *reinterpret_cast<const float4*>(nb + sx);
+  const float4 ny = *reinterpret_cast<const float4*>(nb + 16 + sy);
+  const float4 nz = *reinterpret_cast<const float4*>(nb + 32 + sz);
+  const float4 fx = *reinterpret_cast<const float4*>(nb + 48 - sx);
+  const float4 fy = *reinterpret_cast<const float4*>(nb + 64 - sy);
+  const float4 fz = *reinterpret_cast<const float4*>(nb + 80 - sz);
   if (COUNT) cnt.box += 4;
   const f2 ix = {t.inv.x, t.inv.x}, iy = {t.inv.y, t.inv.y}, iz = {t.inv.z, t.inv.z};
   const f2 ox = {t.oi.x, t.oi.x}, oy = {t.oi.y, t.oi.y}, oz = {t.oi.z, t.oi.z};
@@ -501,6 +499,9 @@ __device__ float perlin_turb(const float4* vec, const int32_t* perm, V3 p) {
   return fabsf(accum);
 }
 
+// FULL = false compiles solid and checker textures only (scenes without image / noise textures):
+// the perlin and image paths cost ~12 vector registers the common scenes would otherwise spill.
+template <bool FULL>
 __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3 p) {
   for (int guard = 0; guard < kMaxTexNesting; ++guard) {
     const float4 t0 = S.textures[tex * 2];
@@ -516,7 +517,7 @@ __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3
       tex = even ? ibits(t0.y) : ibits(t0.z);
       continue;
     }
-    if (type == RTG_TEX_IMAGE) {
+    if (FULL && type == RTG_TEX_IMAGE) {
       const int img = ibits(t1.w);
       if (img < 0) return v3(0.0f, 1.0f, 1.0f);
       const int4 h = S.images[img];
@@ -533,7 +534,7 @@ __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3
       const float cs = 1.0f / 255.0f;
       return v3(cs * px[0], cs * px[1], cs * px[2]);
     }
-    if (type == RTG_TEX_NOISE) {
+    if (FULL && type == RTG_TEX_NOISE) {
       const int pt = ibits(t1.w);
       const float4* vec = S.perlin_vec + pt * 256;
       const int32_t* perm = S.perlin_perm + pt * 768;
@@ -587,6 +588,7 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
 
 // Shades the closest hit `ref` at distance t; returns false when the path ends
 // (ray_color's emission-only return, camera.hpp:213-216, or a miss handled by the caller).
+template <bool FULL>
 __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   V3 p, outward;
   float u = 0.0f, v = 0.0f;
@@ -628,7 +630,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
 
   if (type == RTG_MAT_DIFFUSE_LIGHT) {
     if (needs_uv) sphere_uv();
-    const V3 e = texture_value(S, tex, u, v, p);
+    const V3 e = texture_value<FULL>(S, tex, u, v, p);
     ps.L = add(ps.L, mul(ps.T, e));
     return false;
   }
@@ -642,7 +644,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
       const float s = 1e-8f;
       if (fabsf(dir.x) < s && dir.y < s && fabsf(dir.z) < s) dir = n;
       if (needs_uv) sphere_uv();
-      att = texture_value(S, tex, u, v, p);
+      att = texture_value<FULL>(S, tex, u, v, p);
     } else {
       const V3 in = ps.d;
       const V3 refl = sub(in, scl(2.0f * dot(in, n), n));
@@ -753,12 +755,14 @@ __device__ __forceinline__ void store_pixel(const DevCamera& C, const DevJob& J,
 // longer waits for its slowest traversal before shading, and lanes still traversing keep their
 // stack and continue afterwards. Shaded lanes regenerate their path (next bounce or next sample
 // of the same pixel, in sample order) and re-enter traversal.
-template <int STACK, bool COUNT, int WIDE>
+// The tile coordinates are wave-uniform (scalar registers); the lane's pixel is recomputed from
+// them where needed instead of being kept live in vector registers across the loop.
+template <int STACK, bool COUNT, int WIDE, bool TEXF>
 __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                            const LanePixel& px, int32_t* stk,
-                                            WaveStats<COUNT>& w) {
+                                            int tx, int ty, int32_t* stk, WaveStats<COUNT>& w) {
   V3 acc = v3(0.0f, 0.0f, 0.0f);
   int sample = 0;
+  const LanePixel px = tile_pixel(C, J, tx, ty, __lane_id());
   bool done = !(px.valid && C.max_depth > 0 && C.spp > 0);
   PathState ps;
   Trav tr;
@@ -815,14 +819,15 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
         alive_path = false;
       } else {
         if (COUNT) ++w.hits;
-        alive_path = shade(S, ps, tr.best, tr.tbest);
+        alive_path = shade<TEXF>(S, ps, tr.best, tr.tbest);
         if (alive_path && --ps.depth <= 0) alive_path = false;
       }
       if (!alive_path) {
         acc = add(acc, ps.L);
         ++sample;
         if (sample < C.spp) {
-          start_sample(ps, C, J.seed_mix, px.pixel_id, sample, px.i, px.j);
+          const LanePixel p = tile_pixel(C, J, tx, ty, __lane_id());
+          start_sample(ps, C, J.seed_mix, p.pixel_id, sample, p.i, p.j);
         } else {
           done = true;
         }
@@ -831,18 +836,19 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
     }
     if (COUNT) w.diag[6] += __builtin_amdgcn_s_memtime() - t_shade0;
   }
-  store_pixel(C, J, px, acc);
+  store_pixel(C, J, tile_pixel(C, J, tx, ty, __lane_id()), acc);
 }
 
 // Schedule 0 on a plain grid (one wave = one 8x8 tile, 256-thread workgroups).
-template <int STACK, bool COUNT, int WIDE>
+template <int STACK, bool COUNT, int WIDE, bool TEXF>
 __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
   __shared__ int32_t s_stack[4 * STACK * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int32_t* stk = s_stack + wave * STACK * 64 + lane;
   WaveStats<COUNT> w;
-  render_tile<STACK, COUNT, WIDE>(S, C, J, lane_pixel(C, J, lane, wave), stk, w);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  render_tile<STACK, COUNT, WIDE, TEXF>(S, C, J, blockIdx.x * 2 + (wv & 1), blockIdx.y * 2 + (wv >> 1), stk, w);
   flush_stats<COUNT>(J, w, lane);
 }
 
@@ -851,7 +857,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
 // L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
 // left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
-template <int STACK, bool COUNT, int WAVES, int WIDE>
+template <int STACK, bool COUNT, int WAVES, int WIDE, bool TEXF>
 __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63;
@@ -882,11 +888,11 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   for (;;) {
     int tile = 0;
     if (lane == 0) tile = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
-    tile = __shfl(tile, 0, 64);
+    tile = __builtin_amdgcn_readfirstlane(__shfl(tile, 0, 64));
     if (tile >= J.num_tiles) break;
     const int ty = tile / J.tiles_x;
     const int tx = tile - ty * J.tiles_x;
-    render_tile<STACK, COUNT, WIDE>(L, C, J, tile_pixel(C, J, tx, ty, lane), stk, w);
+    render_tile<STACK, COUNT, WIDE, TEXF>(L, C, J, tx, ty, stk, w);
   }
   flush_stats<COUNT>(J, w, lane);
 }
@@ -920,7 +926,7 @@ __global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCame
       alive = false;
     } else {
       if (COUNT) ++hits;
-      alive = shade(S, ps, tr.best, tr.tbest);
+      alive = shade<true>(S, ps, tr.best, tr.tbest);
       if (alive && --ps.depth <= 0) alive = false;
     }
     if (!alive) {
@@ -972,7 +978,7 @@ __global__ __launch_bounds__(256) void render_kernel_v0(DevScene S, DevCamera C,
       alive = false;
     } else {
       if (COUNT) ++hits;
-      alive = shade(S, ps, ref, t);
+      alive = shade<true>(S, ps, ref, t);
       if (alive && --ps.depth <= 0) alive = false;
     }
     if (!alive) {
@@ -1016,43 +1022,51 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
-template <int STACK, int WIDE>
+template <int STACK, int WIDE, bool TEXF>
 hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                       int lds_bytes, int grid_blocks, hipStream_t stream) {
-  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, true, kLdsWaves, WIDE>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, false, kLdsWaves, WIDE>);
+  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, true, kLdsWaves, WIDE, TEXF>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, false, kLdsWaves, WIDE, TEXF>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (count)
-    hipLaunchKernelGGL((render_kernel_lds<STACK, true, kLdsWaves, WIDE>), dim3(grid_blocks),
+    hipLaunchKernelGGL((render_kernel_lds<STACK, true, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
                        dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel_lds<STACK, false, kLdsWaves, WIDE>), dim3(grid_blocks),
+    hipLaunchKernelGGL((render_kernel_lds<STACK, false, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
                        dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   return hipGetLastError();
 }
 
-template <int STACK, int WIDE>
+template <int STACK, int WIDE, bool TEXF>
 hipError_t launch_plain(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                         hipStream_t stream) {
   const dim3 block(256);
   const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
   if (count)
-    hipLaunchKernelGGL((render_kernel<STACK, true, WIDE>), grid, block, 0, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel<STACK, true, WIDE, TEXF>), grid, block, 0, stream, S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel<STACK, false, WIDE>), grid, block, 0, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel<STACK, false, WIDE, TEXF>), grid, block, 0, stream, S, C, J);
   return hipGetLastError();
+}
+
+template <int STACK, int WIDE>
+hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
+                          bool lds, int lds_bytes, int grid_blocks, hipStream_t stream) {
+  if (lds)
+    return S.tex_full ? launch_lds<STACK, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
+                      : launch_lds<STACK, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+  return S.tex_full ? launch_plain<STACK, WIDE, true>(S, C, J, count, stream)
+                    : launch_plain<STACK, WIDE, false>(S, C, J, count, stream);
 }
 
 template <int STACK>
 hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                         int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
   const bool wide = S.node_width == 4;
-  if (variant == 3)
-    return wide ? launch_lds<STACK, 4>(S, C, J, count, lds_bytes, grid_blocks, stream)
-                : launch_lds<STACK, 2>(S, C, J, count, lds_bytes, grid_blocks, stream);
-  if (variant == 0)
-    return wide ? launch_plain<STACK, 4>(S, C, J, count, stream) : launch_plain<STACK, 2>(S, C, J, count, stream);
+  if (variant == 3 || variant == 0)
+    return wide ? launch_default<STACK, 4>(S, C, J, count, variant == 3, lds_bytes, grid_blocks, stream)
+                : launch_default<STACK, 2>(S, C, J, count, variant == 3, lds_bytes, grid_blocks, stream);
   if (wide) return hipErrorInvalidValue;  // schedules 1 and 2 traverse binary nodes only
   const dim3 block(256);
   const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);

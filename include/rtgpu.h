@@ -160,6 +160,17 @@ typedef struct rtg_camera_params {
 #define RTG_RENDER_SHADE_BATCH(n) (((n) & 0xff) << 16)
 #define RTG_RENDER_LEAF_BATCH(n) (((n) & 0x7f) << 24) /* bits 24-30: leaf batch in lanes (0 = default) */
 
+/* rtg-f32 per-pixel accumulation (DESIGN.md §4 "sample chunks"): a pixel's samples are summed in
+ * chunks of K = rtg_chunk_samples(spp) consecutive samples, each chunk in sample order starting from
+ * zero, and the chunk sums are then added in chunk order; the pixel is pixel_samples_scale * that.
+ * spp <= 64 gives one chunk, i.e. the reference's single running sum (camera.hpp:55-62). Chunks are
+ * the device's unit of work, so one expensive pixel never holds a wavefront for all its samples. */
+static inline int rtg_chunk_samples(int spp) {
+  int n = (spp + 63) / 64;
+  if (n < 1) n = 1;
+  return spp > 0 ? (spp + n - 1) / n : 1;
+}
+
 typedef struct rtg_render_desc {
   uint64_t seed;      /* run seed of the counter RNG */
   int32_t row_begin;  /* first image row of this shard */

@@ -1081,10 +1081,18 @@ int orc_render_f32(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint64_t
     int j = row_begin + r * row_stride;
     for (int i = 0; i < cp.image_width; ++i) {
       uint32_t pid = (uint32_t)j * (uint32_t)cp.image_width + (uint32_t)i;
+      /* rtg-f32 accumulation (rtgpu.h rtg_chunk_samples): chunks of K samples summed from zero in
+         sample order, chunk sums added in chunk order; one chunk == the reference's running sum */
       f3 acc = F3(0.0f, 0.0f, 0.0f);
-      if (cam->max_depth > 0)
-        for (int smp = 0; smp < cam->samples_per_pixel; ++smp)
-          acc = fv_add(acc, sample32(&w, cam, cf, seed, pid, (uint32_t)smp, i, j, &segs));
+      if (cam->max_depth > 0) {
+        int spp = cam->samples_per_pixel, K = rtg_chunk_samples(spp);
+        for (int c0 = 0; c0 < spp; c0 += K) {
+          f3 part = F3(0.0f, 0.0f, 0.0f);
+          for (int smp = c0; smp < spp && smp < c0 + K; ++smp)
+            part = fv_add(part, sample32(&w, cam, cf, seed, pid, (uint32_t)smp, i, j, &segs));
+          acc = c0 == 0 ? part : fv_add(acc, part);
+        }
+      }
       float* o = out + ((int64_t)r * cp.image_width + i) * 3;
       o[0] = scale * acc.x;
       o[1] = scale * acc.y;

@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -16,6 +17,8 @@
 
 namespace rtg {
 int kernel_stack_depth(int bvh_depth);
+hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,
+                          hipStream_t stream);
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
                          bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream);
 int lds_layout(const DevScene& S, int stack, int waves, DevJob* J);
@@ -707,6 +710,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (rows > reachable) return fail(RTG_E_INVALID, "row_count reaches past the image");
   if (static_cast<int64_t>(W) * H >= (int64_t(1) << 32))
     return fail(RTG_E_INVALID, "image larger than 2^32 pixels");
+  if (W > 65535 || rows > 65535)  // the kernels pack a lane's pixel as 16-bit column / row
+    return fail(RTG_E_INVALID, "image width or shard rows above 65535");
 
   DevCamera dc{};
   for (int k = 0; k < 3; ++k) {
@@ -744,6 +749,9 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dj.out = dout;
   dj.tiles_x = (W + 7) / 8;
   dj.num_tiles = dj.tiles_x * ((rows + 7) / 8);
+  dj.chunk_samples = rtg_chunk_samples(cam->samples_per_pixel);
+  dj.chunks = cam->samples_per_pixel > 0 ? (cam->samples_per_pixel + dj.chunk_samples - 1) / dj.chunk_samples : 1;
+  dj.partial = nullptr;
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
   const int lds_bytes = lds_layout(s->dev, s->info.stack_depth, kLdsWaves, &dj);
@@ -756,11 +764,42 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const int grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
   dj.counters = s->counters;
   RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  // optional per-wave timeline for schedule analysis (tools/wave_trace.py)
+  const char* trace_path = std::getenv("RTG_WAVE_TRACE");
+  int64_t trace_slots = 0;
+  if (trace_path) {
+    trace_slots = variant == 3 ? int64_t(grid_blocks) * kLdsWaves
+                               : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
+    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.trace), trace_slots * 32, stream), "hipMalloc(trace)");
+    RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
+  }
+  const bool chunked = dj.chunks > 1 && (variant == 3 || variant == 0) && dc.max_depth > 0;
+  if (chunked)
+    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.partial), out_bytes * dj.chunks, stream),
+            "hipMallocAsync(partial sums)");
+  if (!(variant == 3 || variant == 0)) {  // schedules 1 and 2 keep one running sum per pixel
+    dj.chunks = 1;
+    dj.chunk_samples = std::max(1, cam->samples_per_pixel);
+  }
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
   RTG_HIP(launch_render(s->dev, dc, dj, s->info.stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
                         variant, lds_bytes, grid_blocks, stream),
           "render kernel launch");
+  if (chunked)
+    RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, dj.chunks, dc.scale, stream),
+            "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
+  if (chunked) RTG_HIP(hipFreeAsync(dj.partial, stream), "hipFreeAsync(partial sums)");
+  if (trace_path) {
+    std::vector<unsigned long long> tr(static_cast<size_t>(trace_slots) * 4);
+    RTG_HIP(hipMemcpyAsync(tr.data(), dj.trace, trace_slots * 32, hipMemcpyDeviceToHost, stream), "trace copy");
+    RTG_HIP(hipStreamSynchronize(stream), "trace sync");
+    RTG_HIP(hipFree(dj.trace), "trace free");
+    if (FILE* f = std::fopen(trace_path, "wb")) {
+      std::fwrite(tr.data(), 8, tr.size(), f);
+      std::fclose(f);
+    }
+  }
   RTG_HIP(hipMemcpyAsync(s->host_counters, s->counters, kNumCounters * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, stream),
           "hipMemcpyAsync(counters)");

@@ -137,7 +137,13 @@ struct DevJob {
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 8x8 pixel tiles per shard row of tiles
-  int32_t num_tiles;  // 8x8 pixel tiles in the shard
+  int32_t num_tiles;  // 8x8 pixel tiles in the shard; work is handed out in 4x4 quarters of them
+  int32_t chunks;         // sample chunks per pixel (work units = pixel x chunk), >= 1
+  int32_t chunk_samples;  // K: samples per chunk (the last chunk may be shorter)
+  float* partial;         // chunks > 1: [chunk][row][column][3] partial sums; else null
+  // optional per-wave timeline (RTG_WAVE_TRACE, tools/wave_trace.py): 4 x u64 per wave =
+  // {s_memrealtime at start, at end, pixels finished, block << 8 | wave}; null when off
+  unsigned long long* trace;
   // persistent LDS kernel: byte offsets of the scene copies in dynamic LDS
   int32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_materials, lds_textures;
 };

@@ -160,7 +160,8 @@ struct Counts {
 // -> aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
 // traversal: the nearer child first, the farther one pushed on the lane's LDS stack.
 struct Trav {
-  V3 inv, oi;     // 1/d and -o/d for the fused slab test
+  float ix, iy, iz;  // 1/d
+  float ox, oy, oz;  // -o/d, for the fused slab test
   float tbest;    // closest hit so far (the shrinking interval.max of the reference)
   int32_t best;   // primitive ref of the closest hit, -1 = none
   int32_t todo;   // inner node (>= 0: index, or byte offset in 4-wide trees) or leaf code (< 0)
@@ -169,8 +170,12 @@ struct Trav {
 };
 
 __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d) {
-  t.inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y), __builtin_amdgcn_rcpf(d.z));
-  t.oi = v3(-o.x * t.inv.x, -o.y * t.inv.y, -o.z * t.inv.z);
+  t.ix = __builtin_amdgcn_rcpf(d.x);
+  t.iy = __builtin_amdgcn_rcpf(d.y);
+  t.iz = __builtin_amdgcn_rcpf(d.z);
+  t.ox = -o.x * t.ix;
+  t.oy = -o.y * t.iy;
+  t.oz = -o.z * t.iz;
   t.tbest = __builtin_inff();
   t.best = -1;
   t.todo = 0;
@@ -201,7 +206,7 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, int32_t* s
   const float4 a = n[0], b = n[1], c = n[2];
   const int4 ch = *reinterpret_cast<const int4*>(n + 3);
   if (COUNT) cnt.box += 2;
-  const V3 inv = t.inv, oi = t.oi;
+  const V3 inv = v3(t.ix, t.iy, t.iz), oi = v3(t.ox, t.oy, t.oz);
   // left box lo=(a.x,a.y,a.z) hi=(a.w,b.x,b.y); right lo=(b.z,b.w,c.x) hi=(c.y,c.z,c.w)
   const float l0x = fmaf(a.x, inv.x, oi.x), l1x = fmaf(a.w, inv.x, oi.x);
   const float l0y = fmaf(a.y, inv.y, oi.y), l1y = fmaf(b.x, inv.y, oi.y);
@@ -271,9 +276,9 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* 
     return;
   }
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
-  const int32_t sx = (static_cast<uint32_t>(ibits(t.inv.x)) >> 31) * 48;
-  const int32_t sy = (static_cast<uint32_t>(ibits(t.inv.y)) >> 31) * 48;
-  const int32_t sz = (static_cast<uint32_t>(ibits(t.inv.z)) >> 31) * 48;
+  const int32_t sx = (static_cast<uint32_t>(ibits(t.ix)) >> 31) * 48;
+  const int32_t sy = (static_cast<uint32_t>(ibits(t.iy)) >> 31) * 48;
+  const int32_t sz = (static_cast<uint32_t>(ibits(t.iz)) >> 31) * 48;
   const float4 nx = *reinterpret_cast<const float4*>(nb + sx);
   const float4 ny = *reinterpret_cast<const float4*>(nb + 16 + sy);
   const float4 nz = *reinterpret_cast<const float4*>(nb + 32 + sz);
@@ -281,8 +286,8 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* 
   const float4 fy = *reinterpret_cast<const float4*>(nb + 64 - sy);
   const float4 fz = *reinterpret_cast<const float4*>(nb + 80 - sz);
   if (COUNT) cnt.box += 4;
-  const f2 ix = {t.inv.x, t.inv.x}, iy = {t.inv.y, t.inv.y}, iz = {t.inv.z, t.inv.z};
-  const f2 ox = {t.oi.x, t.oi.x}, oy = {t.oi.y, t.oi.y}, oz = {t.oi.z, t.oi.z};
+  const f2 ix = {t.ix, t.ix}, iy = {t.iy, t.iy}, iz = {t.iz, t.iz};
+  const f2 ox = {t.ox, t.ox}, oy = {t.oy, t.oy}, oz = {t.oz, t.oz};
   const f2 nx01 = pk_fma(f2{nx.x, nx.y}, ix, ox), nx23 = pk_fma(f2{nx.z, nx.w}, ix, ox);
   const f2 ny01 = pk_fma(f2{ny.x, ny.y}, iy, oy), ny23 = pk_fma(f2{ny.z, ny.w}, iy, oy);
   const f2 nz01 = pk_fma(f2{nz.x, nz.y}, iz, oz), nz23 = pk_fma(f2{nz.z, nz.w}, iz, oz);
@@ -715,11 +720,24 @@ __device__ __forceinline__ LanePixel lane_pixel(const DevCamera& C, const DevJob
 // Per-wave accumulators that outlive one tile.
 template <bool COUNT>
 struct WaveStats {
-  uint32_t segs = 0, hits = 0;
+  uint32_t segs = 0, hits = 0, pixels = 0;
   Counts<COUNT> cnt;
   bool overflow = false, corrupt = false;
   uint64_t diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform schedule diagnostics (COUNT only)
 };
+
+__device__ __forceinline__ void trace_wave(const DevJob& J, uint64_t t0, uint32_t pixels, int lane,
+                                           int slot, int tag) {
+  if (J.trace == nullptr) return;
+  const uint32_t wp = wave_sum(pixels);
+  if (lane == 0) {
+    unsigned long long* r = J.trace + static_cast<int64_t>(slot) * 4;
+    r[0] = t0;
+    r[1] = __builtin_amdgcn_s_memrealtime();
+    r[2] = wp;
+    r[3] = static_cast<unsigned long long>(tag);
+  }
+}
 
 template <bool COUNT>
 __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w, int lane) {
@@ -749,31 +767,97 @@ __device__ __forceinline__ void store_pixel(const DevCamera& C, const DevJob& J,
   }
 }
 
-// One wave renders every sample of its 8x8 pixel tile with the ballot-batched schedule: every
-// lane advances its own traversal one step per trip; the wave switches to shading only once at
-// least ceil(alive * shade_batch / 64) lanes have finished their closest-hit query, so a wave no
-// longer waits for its slowest traversal before shading, and lanes still traversing keep their
-// stack and continue afterwards. Shaded lanes regenerate their path (next bounce or next sample
-// of the same pixel, in sample order) and re-enter traversal.
-// The tile coordinates are wave-uniform (scalar registers); the lane's pixel is recomputed from
-// them where needed instead of being kept live in vector registers across the loop.
+// A lane's pixel, packed: column in the low 16 bits, shard-local row in the high 16 bits.
+__device__ __forceinline__ int px_i(uint32_t px) { return static_cast<int>(px & 0xffffu); }
+__device__ __forceinline__ int px_lr(uint32_t px) { return static_cast<int>(px >> 16); }
+
+__device__ __forceinline__ void start_pixel_sample(PathState& ps, const DevCamera& C, const DevJob& J,
+                                                   uint32_t px, uint32_t sample) {
+  const int i = px_i(px);
+  const int j = J.row_begin + px_lr(px) * J.row_stride;
+  const uint32_t pixel_id = static_cast<uint32_t>(j) * static_cast<uint32_t>(C.width) + static_cast<uint32_t>(i);
+  start_sample(ps, C, J.seed_mix, pixel_id, sample, i, j);
+}
+
+// One wave renders a stream of work units with the ballot-batched schedule. A unit is one pixel
+// and one chunk of its samples: samples [c*K, min((c+1)*K, spp)) of chunk c (DESIGN.md §4 "sample
+// chunks"); a lane walks the chunk's samples in order, accumulating them from zero, and stores the
+// chunk's partial sum (or the pixel, when the pixel has one chunk). Units are handed out in batches
+// = (8x8 tile, chunk) from the launch-wide atomic counter J.counters[6], tile-major, so the 64 units
+// of a batch, and the next batch (same tile, next chunk), share one tile: a lane that finishes its
+// unit takes the next unit of the wave's current batch, and the wave takes a new batch once its
+// batch is handed out. Lanes only idle once the whole shard has been handed out, a wave holds at most
+// 63 unstarted units then, and no single expensive pixel (a glass sphere seen through 50 bounces)
+// can hold a wave for more than K samples.
+// Within a loop trip every lane advances its own traversal one step; a trip is either a node step
+// or a leaf step for the whole wave (leaf work waits until leaf_batch lanes have reached a leaf);
+// the wave switches to shading once ceil(alive * shade_batch / 64) lanes have finished their
+// closest-hit query, and lanes still traversing keep their stack and continue afterwards.
 template <int STACK, bool COUNT, int WIDE, bool TEXF>
-__device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                            int tx, int ty, int32_t* stk, WaveStats<COUNT>& w) {
+__device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
+                                              int32_t* stk, WaveStats<COUNT>& w) {
+  const int lane = __lane_id();
+  const bool no_work = C.max_depth <= 0 || C.spp <= 0;  // every pixel is black (camera.hpp:192)
+  const int num_batches = J.num_tiles * J.chunks;
   V3 acc = v3(0.0f, 0.0f, 0.0f);
-  int sample = 0;
-  const LanePixel px = tile_pixel(C, J, tx, ty, __lane_id());
-  bool done = !(px.valid && C.max_depth > 0 && C.spp > 0);
-  PathState ps;
-  Trav tr;
+  uint32_t px = 0;
+  int sample = 0, s_end = 0, chunk = 0;
+  bool has = false;
+  // wave-uniform: the current batch's tile origin and chunk, and its next unassigned unit
+  int bx = 0, by = 0, bc = 0, k_next = 64;
+  bool exhausted = false;
+  PathState ps = {};
+  Trav tr = {};
   tr.active = false;
-  if (!done) {
-    start_sample(ps, C, J.seed_mix, px.pixel_id, 0, px.i, px.j);
-    trav_begin(tr, S, ps.o, ps.d);
-  }
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   for (;;) {
-    const int alive = __popcll(__ballot(!done));
+    // hand the next units of the current batch (new batches as needed) to the lanes without one
+    uint64_t want = __ballot(!has);
+    while (want != 0 && !exhausted) {
+      if (k_next >= 64) {
+        int b = 0;
+        if (lane == 0) b = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
+        b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
+        if (b >= num_batches) {
+          exhausted = true;
+          break;
+        }
+        const int tile = b / J.chunks;
+        bc = b - tile * J.chunks;
+        const int ty = tile / J.tiles_x;
+        bx = (tile - ty * J.tiles_x) * 8;
+        by = ty * 8;
+        k_next = 0;
+      }
+      const int take = min(__popcll(want), 64 - k_next);
+      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+          static_cast<uint32_t>(want >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(want), 0u)));
+      if (!has && rank < take) {
+        const int k = k_next + rank;
+        const int i = bx + (k & 7);
+        const int lr = by + (k >> 3);
+        if (i < C.width && lr < J.row_count) {
+          px = static_cast<uint32_t>(i) | (static_cast<uint32_t>(lr) << 16);
+          if (no_work) {
+            if (bc == 0) {
+              float* o = J.out + (static_cast<int64_t>(lr) * C.width + i) * 3;
+              o[0] = o[1] = o[2] = 0.0f;
+            }
+          } else {
+            has = true;
+            chunk = bc;
+            sample = bc * J.chunk_samples;
+            s_end = min(sample + J.chunk_samples, C.spp);
+            acc = v3(0.0f, 0.0f, 0.0f);
+            start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
+            trav_begin(tr, S, ps.o, ps.d);
+          }
+        }
+      }
+      k_next += take;
+      want = __ballot(!has);
+    }
+    const int alive = __popcll(__ballot(has));
     if (alive == 0) break;
     const int need = (alive * J.shade_batch + 63) >> 6;
     uint64_t t_trav0 = 0;
@@ -782,11 +866,8 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
       if (COUNT) {
         w.diag[0] += 1;
         w.diag[1] += __popcll(__ballot(tr.active));
-        w.diag[2] += __popcll(__ballot(done));
+        w.diag[2] += __popcll(__ballot(!has));
       }
-      // A trip is either a node step or a leaf step for the whole wave, never both: leaf work
-      // (primitive tests) waits until leaf_batch lanes have reached a leaf or no lane has an
-      // inner node left, so the expensive primitive tests run with the lanes batched.
       const int at_leaf = __popcll(__ballot(tr.active && tr.todo < 0));
       const bool inner_left = __ballot(tr.active && tr.todo >= 0) != 0;
       if (at_leaf >= J.leaf_batch || !inner_left) {
@@ -801,7 +882,7 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
         }
       }
       const uint64_t trav = __ballot(tr.active);
-      const int ready = __popcll(__ballot(!tr.active && !done));
+      const int ready = __popcll(__ballot(!tr.active && has));
       if (trav == 0 || ready >= need) break;
     }
     uint64_t t_shade0 = 0;
@@ -809,9 +890,9 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
       t_shade0 = __builtin_amdgcn_s_memtime();
       w.diag[5] += t_shade0 - t_trav0;
       w.diag[3] += 1;
-      w.diag[4] += __popcll(__ballot(!tr.active && !done));
+      w.diag[4] += __popcll(__ballot(!tr.active && has));
     }
-    if (!tr.active && !done) {
+    if (!tr.active && has) {
       ++w.segs;
       bool alive_path;
       if (tr.best < 0) {
@@ -825,31 +906,45 @@ __device__ __forceinline__ void render_tile(const DevScene& S, const DevCamera& 
       if (!alive_path) {
         acc = add(acc, ps.L);
         ++sample;
-        if (sample < C.spp) {
-          const LanePixel p = tile_pixel(C, J, tx, ty, __lane_id());
-          start_sample(ps, C, J.seed_mix, p.pixel_id, sample, p.i, p.j);
+        if (sample < s_end) {
+          start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
         } else {
-          done = true;
+          const int64_t pix = static_cast<int64_t>(px_lr(px)) * C.width + px_i(px);
+          if (J.partial == nullptr) {  // one chunk per pixel: the pixel mean directly
+            float* o = J.out + pix * 3;
+            o[0] = C.scale * acc.x;
+            o[1] = C.scale * acc.y;
+            o[2] = C.scale * acc.z;
+          } else {  // chunk partial sum, combined in chunk order by combine_kernel
+            float* o = J.partial + (static_cast<int64_t>(chunk) * J.row_count * C.width + pix) * 3;
+            o[0] = acc.x;
+            o[1] = acc.y;
+            o[2] = acc.z;
+          }
+          has = false;
+          ++w.pixels;
         }
       }
-      if (!done) trav_begin(tr, S, ps.o, ps.d);
+      if (has) trav_begin(tr, S, ps.o, ps.d);
     }
     if (COUNT) w.diag[6] += __builtin_amdgcn_s_memtime() - t_shade0;
   }
-  store_pixel(C, J, tile_pixel(C, J, tx, ty, __lane_id()), acc);
 }
 
-// Schedule 0 on a plain grid (one wave = one 8x8 tile, 256-thread workgroups).
+// Schedule 4: the same loop on a plain grid of 256-thread workgroups (scene read through the
+// caches; used when it does not fit in LDS). Waves take tiles from the same counter.
 template <int STACK, bool COUNT, int WIDE, bool TEXF>
 __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
   __shared__ int32_t s_stack[4 * STACK * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int32_t* stk = s_stack + wave * STACK * 64 + lane;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   WaveStats<COUNT> w;
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  render_tile<STACK, COUNT, WIDE, TEXF>(S, C, J, blockIdx.x * 2 + (wv & 1), blockIdx.y * 2 + (wv >> 1), stk, w);
+  render_stream<STACK, COUNT, WIDE, TEXF>(S, C, J, stk, w);
   flush_stats<COUNT>(J, w, lane);
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  trace_wave(J, t0, w.pixels, lane, blk * 4 + wave, (blk << 8) | wave);
 }
 
 // Schedule 3 (default when the geometry fits): persistent workgroups of WAVES waves, one per CU.
@@ -860,6 +955,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 template <int STACK, bool COUNT, int WAVES, int WIDE, bool TEXF>
 __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
@@ -885,16 +981,9 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   L.materials = l_materials;
   L.textures = l_textures;
   WaveStats<COUNT> w;
-  for (;;) {
-    int tile = 0;
-    if (lane == 0) tile = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
-    tile = __builtin_amdgcn_readfirstlane(__shfl(tile, 0, 64));
-    if (tile >= J.num_tiles) break;
-    const int ty = tile / J.tiles_x;
-    const int tx = tile - ty * J.tiles_x;
-    render_tile<STACK, COUNT, WIDE, TEXF>(L, C, J, tx, ty, stk, w);
-  }
+  render_stream<STACK, COUNT, WIDE, TEXF>(L, C, J, stk, w);
   flush_stats<COUNT>(J, w, lane);
+  trace_wave(J, t0, w.pixels, lane, blockIdx.x * WAVES + wave, (blockIdx.x << 8) | wave);
 }
 
 // Schedule 1: each loop trip runs one complete closest-hit query per lane through trav_step, so
@@ -1020,6 +1109,16 @@ __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ 
   out[k] = static_cast<uint8_t>(static_cast<int>(256.0f * x));
 }
 
+// Pixel = scale * (((p_0 + p_1) + p_2) + ...): the chunk partial sums in chunk order.
+__global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ partial, float* __restrict__ out,
+                                                      int64_t n_pixels, int chunks, float scale) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n_pixels * 3) return;
+  float acc = partial[k];
+  for (int c = 1; c < chunks; ++c) acc = acc + partial[static_cast<int64_t>(c) * n_pixels * 3 + k];
+  out[k] = scale * acc;
+}
+
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
 template <int STACK, int WIDE, bool TEXF>
@@ -1135,6 +1234,14 @@ hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J,
     default:
       return hipErrorInvalidValue;
   }
+}
+
+hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,
+                          hipStream_t stream) {
+  if (n_pixels <= 0) return hipSuccess;
+  const unsigned blocks = static_cast<unsigned>((n_pixels * 3 + 255) / 256);
+  hipLaunchKernelGGL(combine_kernel, dim3(blocks), dim3(256), 0, stream, partial, out, n_pixels, chunks, scale);
+  return hipGetLastError();
 }
 
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream) {

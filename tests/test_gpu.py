@@ -141,6 +141,19 @@ def test_shards_and_determinism(gpu_lib, scenes):
     ds.close()
 
 
+@pytest.mark.parametrize("spp", [65, 130, 200])
+def test_sample_chunks_match_oracle(gpu_lib, scenes, oracle, spp):
+    """Above 64 spp a pixel's samples are accumulated in chunks (rtgpu.h rtg_chunk_samples) that the
+    device renders as separate work units and combines in chunk order: bit-identical to cpu_ref32."""
+    g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", image_width=48,
+                             samples_per_pixel=spp, max_depth=20)
+    assert rtgpu.chunk_samples(spp) < spp
+    assert_parity(g, o, st, segs)
+    gs, _, _, _ = compare(gpu_lib, scenes, oracle, "bouncing_spheres", image_width=48,
+                          samples_per_pixel=spp, max_depth=20)
+    assert np.array_equal(g, gs)  # deterministic whatever order the units ran in
+
+
 @pytest.mark.parametrize("case", ["one_pixel", "odd_width", "depth0", "depth1", "spp1", "pinhole",
                                   "tall"])
 def test_edge_cases(gpu_lib, scenes, oracle, case):

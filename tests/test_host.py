@@ -20,10 +20,21 @@ def test_cabi_exports_every_declared_symbol(lib):
     with open(os.path.join(REPO, "include", "rtgpu.h")) as f:
         header = f.read()
     declared = set(re.findall(r"^\s*(?:[\w\s\*]+?)\b(rtg_\w+)\s*\(", header, re.M))
+    inline = set(re.findall(r"^static inline \w+ (rtg_\w+)\s*\(", header, re.M))  # header-only rules
+    declared -= inline
     assert declared == set(rtgpu.RTG_SYMBOLS)
     for name in declared:
         assert hasattr(lib.lib, name), name  # dlsym succeeds
     assert lib.lib.rtg_abi_version() == rtgpu.RTG_ABI_VERSION
+
+
+def test_chunk_rule():
+    """rtg_chunk_samples (rtgpu.h): one chunk up to 64 spp, chunks of <= 64 samples above."""
+    def k(spp):
+        n = max(1, (spp + 63) // 64)
+        return (spp + n - 1) // n if spp > 0 else 1
+    assert [k(s) for s in (1, 10, 64, 65, 500, 1000, 2000)] == [1, 10, 64, 33, 63, 63, 63]
+    assert rtgpu.chunk_samples(500) == 63 and rtgpu.chunk_samples(64) == 64
 
 
 def test_scenes_lib_exports(scenes):

@@ -54,8 +54,8 @@ def main():
 
     def scene_for(name, tune):
         if (name, tune) not in scenes:
-            if tune:
-                os.environ["RTG_SAH_TUNE"] = tune
+            if tune.split("@", 1)[0]:
+                os.environ["RTG_SAH_TUNE"] = tune.split("@", 1)[0]
             else:
                 os.environ.pop("RTG_SAH_TUNE", None)
             scenes[(name, tune)] = libs[name].scene_create(s.desc)
@@ -76,6 +76,10 @@ def main():
         for v in variants:
             name, (sched, batch, leaf), tune = v
             L, ds = libs[name], scene_for(name, tune)
+            if "@" in tune:  # "#ct:ml@tile_step" or "#@tile_step": tile visiting step override
+                os.environ["RTG_TILE_STEP"] = tune.split("@", 1)[1]
+            else:
+                os.environ.pop("RTG_TILE_STEP", None)
             flags = rtgpu.RTG_RENDER_OUT_DEVICE | (sched << 8) | (batch << 16) | (leaf << 24)
             job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, flags, stream)
             st = rtgpu.rtg_render_stats()

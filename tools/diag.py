@@ -18,14 +18,17 @@ def main():
     ap.add_argument("--batches", default="48")
     ap.add_argument("--leaf", type=int, default=0)
     ap.add_argument("--schedule", type=int, default=0)
+    ap.add_argument("--lib", default=None, help="librtgpu.so to load (default: the in-tree build)")
+    ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()
     import rtgpu
 
-    lib = rtgpu.Library()
+    lib = rtgpu.Library(os.path.join(REPO, a.lib) if a.lib else None)
     s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
-                                   spp=a.spp, max_depth=50)
+                                   spp=a.spp, max_depth=a.depth)
     ds = lib.scene_create(s.desc)
     out = {}
+    out["lib"] = lib.path
     for b in [int(x) for x in a.batches.split(",")]:
         import ctypes as C
         import numpy as np

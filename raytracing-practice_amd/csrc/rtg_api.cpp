@@ -750,6 +750,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dj.tiles_x = (W + 7) / 8;
   dj.num_tiles = dj.tiles_x * ((rows + 7) / 8);
   dj.chunk_samples = rtg_chunk_samples(cam->samples_per_pixel);
+  // RTG_CHUNK_SAMPLES overrides K for schedule experiments (the frame then differs from the spec)
+  if (const char* e = std::getenv("RTG_CHUNK_SAMPLES")) dj.chunk_samples = std::max(1, std::atoi(e));
   dj.chunks = cam->samples_per_pixel > 0 ? (cam->samples_per_pixel + dj.chunk_samples - 1) / dj.chunk_samples : 1;
   dj.partial = nullptr;
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits

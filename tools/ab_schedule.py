@@ -7,7 +7,8 @@
 Each variant "S:B:L" = schedule S (include/rtgpu.h RTG_RENDER_SCHEDULE) with shade batch B (64ths)
 and leaf batch L (lanes); 0 = library default. A variant may be prefixed "name@" to pick one of
 the --libs builds (default: the first) and suffixed "#ct:ml" to build its BVH with SAH traversal
-cost ct and max leaf size ml (RTG_SAH_TUNE). Renders BASELINE config 2 (book-1, 1920x1080, depth 50)
+cost ct and max leaf size ml (RTG_SAH_TUNE), "#@K" / "#ct:ml@K" to render with K samples per chunk
+(RTG_CHUNK_SAMPLES; the frame then differs from the rtg-f32 spec, for schedule experiments only). Renders BASELINE config 2 (book-1, 1920x1080, depth 50)
 and reports the kernel time (HIP events) per variant per round plus the median Mrays/s; checks
 every variant's frame against the first one (identical, or the fraction of equal pixels).
 """
@@ -66,8 +67,8 @@ def main():
 
     variants = []
     for v in a.variants.split(","):
-        name, spec = (v.split("@", 1) if "@" in v else (first, v))
-        spec, tune = (spec.split("#", 1) if "#" in spec else (spec, ""))
+        head, tune = (v.split("#", 1) if "#" in v else (v, ""))
+        name, spec = (head.split("@", 1) if "@" in head else (first, head))
         nums = tuple(int(x) for x in (spec.split(":") + ["0", "0"])[:3])
         variants.append((name, nums, tune))
     times = {v: [] for v in variants}
@@ -76,10 +77,10 @@ def main():
         for v in variants:
             name, (sched, batch, leaf), tune = v
             L, ds = libs[name], scene_for(name, tune)
-            if "@" in tune:  # "#ct:ml@tile_step" or "#@tile_step": tile visiting step override
-                os.environ["RTG_TILE_STEP"] = tune.split("@", 1)[1]
+            if "@" in tune:  # "#ct:ml@K" or "#@K": samples-per-chunk override (RTG_CHUNK_SAMPLES)
+                os.environ["RTG_CHUNK_SAMPLES"] = tune.split("@", 1)[1]
             else:
-                os.environ.pop("RTG_TILE_STEP", None)
+                os.environ.pop("RTG_CHUNK_SAMPLES", None)
             flags = rtgpu.RTG_RENDER_OUT_DEVICE | (sched << 8) | (batch << 16) | (leaf << 24)
             job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, flags, stream)
             st = rtgpu.rtg_render_stats()

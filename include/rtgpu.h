@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 1
+#define RTG_ABI_VERSION 2
 
 typedef int32_t rtg_status;
 #define RTG_OK 0
@@ -191,8 +191,10 @@ typedef struct rtg_render_stats {
    * [0] traversal trips, [1] lanes stepping summed over trips, [2] lanes idle because their
    * pixel is finished summed over trips, [3] shading trips, [4] lanes shading summed over trips,
    * [5] / [6] shader-clock cycles spent in the traversal / shading phases (s_memtime, all waves),
-   * [7] traversal trips that were leaf trips */
-  uint64_t diag[8];
+   * [7] traversal trips that were leaf trips, [8] shader-clock cycles of the leaf trips,
+   * [9] lanes that ran a node step summed over node trips, [10] lanes that ran a leaf step summed
+   * over leaf trips, [11] reserved */
+  uint64_t diag[12];
 } rtg_render_stats;
 
 typedef struct rtg_scene rtg_scene; /* opaque; owns the device copy of the scene */

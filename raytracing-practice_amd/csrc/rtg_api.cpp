@@ -29,9 +29,9 @@ using namespace rtg;
 
 namespace {
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
-constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
+constexpr int kDefaultLeafBatch = 16;   // lanes waiting at a leaf before a leaf trip
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
-constexpr int kNumCounters = 16;        // [0..6] see DevJob::counters, [8..14] diagnostics
+constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..19] diagnostics
 }
 
 namespace {
@@ -633,7 +633,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.tex_full = 0;
   for (int32_t t = 0; t < desc->num_textures; ++t)
     if (desc->textures[t].type == RTG_TEX_IMAGE || desc->textures[t].type == RTG_TEX_NOISE) s->dev.tex_full = 1;
-  s->dev.pad_ = 0;
+  s->dev.num_perlins = static_cast<int32_t>(hs.perlin_perm.size() / 768);
   s->num_cus = prop.multiProcessorCount;
 
   s->info.device = device;
@@ -685,7 +685,7 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
     stats->hits = c[3];
     stats->samples = s->pending_samples;
     stats->kernel_ms = ms;
-    for (int k = 0; k < 8; ++k) stats->diag[k] = c[8 + k];
+    for (int k = 0; k < 12; ++k) stats->diag[k] = c[8 + k];
   }
   return RTG_OK;
 }

@@ -723,7 +723,7 @@ struct WaveStats {
   uint32_t segs = 0, hits = 0, pixels = 0;
   Counts<COUNT> cnt;
   bool overflow = false, corrupt = false;
-  uint64_t diag[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // wave-uniform schedule diagnostics (COUNT only)
+  uint64_t diag[12] = {};  // wave-uniform schedule diagnostics (COUNT only, rtg_render_stats::diag)
 };
 
 __device__ __forceinline__ void trace_wave(const DevJob& J, uint64_t t0, uint32_t pixels, int lane,
@@ -750,7 +750,7 @@ __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w
       atomicAdd(&J.counters[1], static_cast<unsigned long long>(wbox));
       atomicAdd(&J.counters[2], static_cast<unsigned long long>(wprim));
       atomicAdd(&J.counters[3], static_cast<unsigned long long>(whits));
-      for (int k = 0; k < 8; ++k) atomicAdd(&J.counters[8 + k], static_cast<unsigned long long>(w.diag[k]));
+      for (int k = 0; k < 12; ++k) atomicAdd(&J.counters[8 + k], static_cast<unsigned long long>(w.diag[k]));
     }
   }
   if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
@@ -871,9 +871,16 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       const int at_leaf = __popcll(__ballot(tr.active && tr.todo < 0));
       const bool inner_left = __ballot(tr.active && tr.todo >= 0) != 0;
       if (at_leaf >= J.leaf_batch || !inner_left) {
-        if (COUNT) w.diag[7] += 1;
+        uint64_t tl = 0;
+        if (COUNT) {
+          w.diag[7] += 1;
+          w.diag[10] += at_leaf;
+          tl = __builtin_amdgcn_s_memtime();
+        }
         if (tr.active && tr.todo < 0) leaf_step<COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+        if (COUNT) w.diag[8] += __builtin_amdgcn_s_memtime() - tl;
       } else {
+        if (COUNT) w.diag[9] += __popcll(__ballot(tr.active && tr.todo >= 0));
         if (tr.active && tr.todo >= 0) {
           if constexpr (WIDE == 4)
             node_step4<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
@@ -972,6 +979,12 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
   if (S.ref_mode == 0)
     for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
+  float4* l_pvec = reinterpret_cast<float4*>(smem + J.lds_perlin_vec);
+  int32_t* l_pperm = reinterpret_cast<int32_t*>(smem + J.lds_perlin_perm);
+  if (TEXF) {
+    for (int k = threadIdx.x; k < S.num_perlins * 256; k += WAVES * 64) l_pvec[k] = S.perlin_vec[k];
+    for (int k = threadIdx.x; k < S.num_perlins * 768; k += WAVES * 64) l_pperm[k] = S.perlin_perm[k];
+  }
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
@@ -980,6 +993,10 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   L.quads = l_quads;
   L.materials = l_materials;
   L.textures = l_textures;
+  if (TEXF) {
+    L.perlin_vec = l_pvec;
+    L.perlin_perm = l_pperm;
+  }
   WaveStats<COUNT> w;
   render_stream<STACK, COUNT, WIDE, TEXF>(L, C, J, stk, w);
   flush_stats<COUNT>(J, w, lane);
@@ -1209,6 +1226,10 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
   off = a16(off + int64_t(S.num_materials) * 32);
   const int64_t textures = off;
   off = a16(off + int64_t(S.num_textures) * 32);
+  const int64_t pvec = off;
+  off = a16(off + int64_t(S.num_perlins) * 256 * 16);
+  const int64_t pperm = off;
+  off = a16(off + int64_t(S.num_perlins) * 768 * 4);
   if (off > 160 * 1024) return -1;
   if (J) {
     J->lds_materials = static_cast<int32_t>(materials);
@@ -1217,6 +1238,8 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
     J->lds_spheres = static_cast<int32_t>(spheres);
     J->lds_quads = static_cast<int32_t>(quads);
     J->lds_refs = static_cast<int32_t>(refs);
+    J->lds_perlin_vec = static_cast<int32_t>(pvec);
+    J->lds_perlin_perm = static_cast<int32_t>(pperm);
   }
   return static_cast<int>(off);
 }

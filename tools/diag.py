@@ -50,7 +50,12 @@ def main():
                   "trav_cycles_frac": d[5] / max(1, d[5] + d[6]),
                   "cycles_per_trav_trip": d[5] / max(1, d[0]),
                   "cycles_per_shade_trip": d[6] / max(1, d[3]),
-                  "leaf_trip_frac": d[7] / max(1, d[0])}
+                  "leaf_trip_frac": d[7] / max(1, d[0]),
+                  "leaf_cycles_frac_of_trav": d[8] / max(1, d[5]),
+                  "node_trip_lane_util": d[9] / (64 * max(1, d[0] - d[7])),
+                  "leaf_trip_lane_util": d[10] / (64 * max(1, d[7])),
+                  "node_steps_per_segment": d[9] / st.segments,
+                  "leaf_steps_per_segment": d[10] / st.segments}
     print(json.dumps(out, indent=1))
 
 

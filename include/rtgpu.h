@@ -193,8 +193,10 @@ typedef struct rtg_render_stats {
    * [5] / [6] shader-clock cycles spent in the traversal / shading phases (s_memtime, all waves),
    * [7] traversal trips that were leaf trips, [8] shader-clock cycles of the leaf trips,
    * [9] lanes that ran a node step summed over node trips, [10] lanes that ran a leaf step summed
-   * over leaf trips, [11] reserved */
-  uint64_t diag[12];
+   * over leaf trips; cycles of the shading phase split into [11] miss / material scatter,
+   * [12] path end (sample restart or chunk store), [13] traversal setup of the next segment;
+   * [14], [15] reserved */
+  uint64_t diag[16];
 } rtg_render_stats;
 
 typedef struct rtg_scene rtg_scene; /* opaque; owns the device copy of the scene */

@@ -29,9 +29,9 @@ using namespace rtg;
 
 namespace {
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
-constexpr int kDefaultLeafBatch = 16;   // lanes waiting at a leaf before a leaf trip
+constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
-constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..19] diagnostics
+constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
 }
 
 namespace {
@@ -685,7 +685,7 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
     stats->hits = c[3];
     stats->samples = s->pending_samples;
     stats->kernel_ms = ms;
-    for (int k = 0; k < 12; ++k) stats->diag[k] = c[8 + k];
+    for (int k = 0; k < 16; ++k) stats->diag[k] = c[8 + k];
   }
   return RTG_OK;
 }
@@ -754,6 +754,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (const char* e = std::getenv("RTG_CHUNK_SAMPLES")) dj.chunk_samples = std::max(1, std::atoi(e));
   dj.chunks = cam->samples_per_pixel > 0 ? (cam->samples_per_pixel + dj.chunk_samples - 1) / dj.chunk_samples : 1;
   dj.partial = nullptr;
+
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
   const int lds_bytes = lds_layout(s->dev, s->info.stack_depth, kLdsWaves, &dj);

@@ -133,7 +133,7 @@ struct DevJob {
   int32_t shade_batch;  // schedule 0: shade once ceil(alive * shade_batch / 64) lanes are ready
   float* out;
   // [0] segments, [1] box tests, [2] prim tests, [3] hits, [4] stack overflow, [5] bad BVH code,
-  // [6] persistent kernels' tile counter, [8..19] schedule diagnostics
+  // [6] persistent kernels' tile counter, [8..23] schedule diagnostics
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 8x8 pixel tiles per shard row of tiles
@@ -147,6 +147,7 @@ struct DevJob {
   // persistent LDS kernel: byte offsets of the scene copies in dynamic LDS
   int32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_materials, lds_textures;
   int32_t lds_perlin_vec, lds_perlin_perm;  // noise tables (full-texture kernels only)
+
 };
 
 }  // namespace rtg

@@ -99,7 +99,7 @@ class rtg_render_desc(C.Structure):
 class rtg_render_stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("box_tests", C.c_uint64),
                 ("prim_tests", C.c_uint64), ("hits", C.c_uint64), ("kernel_ms", C.c_double),
-                ("diag", C.c_uint64 * 12)]
+                ("diag", C.c_uint64 * 16)]
 
 
 class rtg_scene_info(C.Structure):

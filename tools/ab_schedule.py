@@ -54,6 +54,7 @@ def main():
     scenes = {}
 
     def scene_for(name, tune):
+        tune = tune.split("%", 1)[0]
         if (name, tune) not in scenes:
             if tune.split("@", 1)[0]:
                 os.environ["RTG_SAH_TUNE"] = tune.split("@", 1)[0]
@@ -77,6 +78,11 @@ def main():
         for v in variants:
             name, (sched, batch, leaf), tune = v
             L, ds = libs[name], scene_for(name, tune)
+            if "%" in tune:  # "...%v": RTG_COMBINE=v
+                os.environ["RTG_COMBINE"] = tune.split("%", 1)[1]
+                tune = tune.split("%", 1)[0]
+            else:
+                os.environ.pop("RTG_COMBINE", None)
             if "@" in tune:  # "#ct:ml@K" or "#@K": samples-per-chunk override (RTG_CHUNK_SAMPLES)
                 os.environ["RTG_CHUNK_SAMPLES"] = tune.split("@", 1)[1]
             else:

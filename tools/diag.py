@@ -55,7 +55,8 @@ def main():
                   "node_trip_lane_util": d[9] / (64 * max(1, d[0] - d[7])),
                   "leaf_trip_lane_util": d[10] / (64 * max(1, d[7])),
                   "node_steps_per_segment": d[9] / st.segments,
-                  "leaf_steps_per_segment": d[10] / st.segments}
+                  "leaf_steps_per_segment": d[10] / st.segments,
+                  "shade_split_scatter_end_setup": [round(d[k] / max(1, d[6]), 3) for k in (11, 12, 13)]}
     print(json.dumps(out, indent=1))
 
 

@@ -27,23 +27,41 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_BOX, BYTES_PER_PRIM, BYTES_PER_HIT = 32, 32, 16  # SURVEY.md §8d algorithmic bytes
 
 
+# BASELINE.json configs (config 1 is the reference's own CPU plumbing run, not a GPU bench line)
+CONFIGS = {
+    2: dict(scene="bouncing_spheres", grid=11, width=1920, height=1080, spp=500, depth=50),
+    3: dict(scene="earth_perlin", grid=0, width=1920, height=1080, spp=500, depth=50),
+    4: dict(scene="cornell_box", grid=0, width=800, height=800, spp=2000, depth=100),
+    5: dict(scene="bouncing_spheres", grid=500, width=3840, height=2160, spp=1000, depth=50),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--scene", default="bouncing_spheres")
-    ap.add_argument("--grid", type=int, default=11, help="bouncing_spheres grid half-width (500 = 1M spheres)")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--spp", type=int, default=500)
-    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="BASELINE.json config preset (2 = the headline metric); flags below override it")
+    ap.add_argument("--scene", default=None)
+    ap.add_argument("--grid", type=int, default=None, help="bouncing_spheres grid half-width (500 = 1M spheres)")
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--bvh", choices=["sah", "median"], default="sah")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU sample")
+    ap.add_argument("--cpu-spp", type=int, default=None,
+                    help="spp of the bounded CPU sample (default 8; 2 for the 4K config 5)")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    return ap.parse_args()
+    a = ap.parse_args()
+    for k, v in CONFIGS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    if a.cpu_spp is None:
+        a.cpu_spp = 2 if a.width * a.height > 4_000_000 else 8
+    return a
 
 
 def cpu_baseline(args, scene_desc, cam):
@@ -55,9 +73,11 @@ def cpu_baseline(args, scene_desc, cam):
     W, H, spp, depth = args.width, args.height, args.cpu_spp, args.depth
     sample = f"{args.scene} {W}x{H}, {spp} spp, depth {depth}, rows dealt over {threads} workers"
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    if args.scene == "bouncing_spheres" and args.grid == 11 and os.access(harness, os.X_OK):
+    # scenes the ref-hybrid harness builds from the reference's own geometry code
+    hscene = {("bouncing_spheres", 11): "book1", ("cornell_box", 0): "cornell"}.get((args.scene, args.grid))
+    if hscene and os.access(harness, os.X_OK):
         try:
-            out = subprocess.run([harness, "bench", "book1", str(W), str(H), str(spp), str(depth),
+            out = subprocess.run([harness, "bench", hscene, str(W), str(H), str(spp), str(depth),
                                   str(threads)], check=True, capture_output=True, text=True,
                                  timeout=600).stdout
             r = json.loads(out)
@@ -177,8 +197,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (the reference's book-1 scene regenerated from glibc rand seed 1)",
-            "config": {"workload": workload, "scene": args.scene, "grid": args.grid, "width": W,
+            "data": ("synthetic (the reference's scene regenerated from glibc rand seed 1"
+                     + (", earthmap texels from tests/golden" if args.scene.startswith("earth") else "") + ")"),
+            "config": {"workload": workload, "baseline_config": args.config, "scene": args.scene,
+                       "grid": args.grid, "width": W,
                        "height": H, "spp": args.spp, "depth": args.depth, "bvh": args.bvh,
                        "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather to rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

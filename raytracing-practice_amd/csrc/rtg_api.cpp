@@ -28,6 +28,8 @@ hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipSt
 using namespace rtg;
 
 namespace {
+constexpr int kMaxStackNeed = 4096;     // traversal stack entries per lane (LDS part + global spill)
+constexpr int kPlainWgsPerCu = 5;        // schedule 4 grid: resident workgroups per CU (waves pull work)
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
 constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
@@ -458,6 +460,7 @@ struct rtg_scene {
   unsigned long long* host_counters = nullptr;  // pinned [8]
   DevScene dev{};
   rtg_scene_info info{};
+  int stack_need = 0;  // structural maximum of traversal stack entries of the BVH
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
@@ -533,10 +536,9 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   HostScene hs;
   std::string err;
   if (!compile_scene(desc, &hs, &err)) return fail(RTG_E_INVALID, err);
-  const int stack = kernel_stack_depth(hs.stack_need);
-  if (stack < 0)
-    return fail(RTG_E_UNSUPPORTED, "BVH needs " + std::to_string(hs.stack_need) +
-                                       " stack entries, more than the deepest kernel stack (64)");
+  if (hs.stack_need > kMaxStackNeed)
+    return fail(RTG_E_UNSUPPORTED, "BVH needs " + std::to_string(hs.stack_need) + " stack entries (limit " +
+                                       std::to_string(kMaxStackNeed) + ")");
   const auto t1 = std::chrono::steady_clock::now();
 
   int ndev = 0;
@@ -641,7 +643,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->info.num_prims = hs.num_prims;
   s->info.num_nodes = hs.num_nodes;
   s->info.bvh_depth = hs.depth;
-  s->info.stack_depth = stack;
+  s->info.stack_depth = hs.stack_need;
+  s->stack_need = hs.stack_need;
   s->info.device_bytes = static_cast<int64_t>(total);
   s->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
   s->info.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
@@ -676,8 +679,6 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   RTG_HIP(hipStreamSynchronize(s->pending_stream), "render stream");
   const unsigned long long* c = s->host_counters;
   s->pending = false;
-  if (c[4] != 0) return fail(RTG_E_UNSUPPORTED, "BVH traversal stack overflow");
-  if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
   if (stats) {
     stats->segments = c[0];
     stats->box_tests = c[1];
@@ -687,6 +688,10 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
     stats->kernel_ms = ms;
     for (int k = 0; k < 16; ++k) stats->diag[k] = c[8 + k];
   }
+  // stats stay filled for diagnosis; the frame is not valid in either case
+  if (c[4] != 0)
+    return fail(RTG_E_UNSUPPORTED, "BVH traversal stack overflow in " + std::to_string(c[4]) + " waves");
+  if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
   return RTG_OK;
 }
 
@@ -757,22 +762,50 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
 
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
-  const int lds_bytes = lds_layout(s->dev, s->info.stack_depth, kLdsWaves, &dj);
+  // traversal stack: 16 LDS entries for the persistent kernel, 16 or 32 for the plain grid (the
+  // most its occupancy allows), deeper BVHs spill the rest to a global per-wave area; the A/B
+  // schedules 1 and 2 keep the whole stack in LDS.
+  const int need = std::max(1, s->stack_need);
+  const int lds_bytes = lds_layout(s->dev, kLdsStack, kLdsWaves, &dj);
   if (variant == 0) variant = lds_bytes > 0 ? 3 : 4;
   if (variant == 5) variant = 3;  // former 16-wave alias
   if (variant == 4) variant = 0;  // plain-grid ballot schedule
   if (variant == 3 && lds_bytes < 0) return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
   if ((variant == 1 || variant == 2) && s->dev.node_width != 2)
     return fail(RTG_E_INVALID, "schedules 1 and 2 need a binary BVH (RTG_BVH_MEDIAN)");
-  const int grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
+  int stack_depth = 0;
+  int grid_blocks = 1, grid_waves = 0;
+  if (variant == 3) {
+    stack_depth = kLdsStack;
+    grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
+    grid_waves = grid_blocks * kLdsWaves;
+  } else if (variant == 0) {
+    stack_depth = need <= 16 ? 16 : 32;
+    grid_blocks = std::max(1, std::min(s->num_cus * kPlainWgsPerCu, (dj.num_tiles + 3) / 4));
+    grid_waves = grid_blocks * 4;
+  } else {
+    stack_depth = kernel_stack_depth(need);
+    if (stack_depth < 0) return fail(RTG_E_UNSUPPORTED, "schedules 1 and 2 support BVH stacks up to 64");
+  }
+  if (const char* e = std::getenv("RTG_STACK")) stack_depth = std::atoi(e);  // experiments only
+  dj.lds_stack = stack_depth;
+  // RTG_STACK_LDS_ENTRIES (tests): keep fewer entries in LDS so the global spill path is exercised
+  if (const char* e = std::getenv("RTG_STACK_LDS_ENTRIES"))
+    dj.lds_stack = std::min(stack_depth, std::max(1, std::atoi(e)));
+  dj.spill_depth = (variant == 3 || variant == 0) ? std::max(0, need - dj.lds_stack) : 0;
+  dj.spill = nullptr;
+  if (dj.spill_depth > 0)
+    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.spill),
+                           static_cast<size_t>(grid_waves) * 64 * dj.spill_depth * sizeof(int32_t), stream),
+            "hipMallocAsync(stack spill)");
   dj.counters = s->counters;
   RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
   // optional per-wave timeline for schedule analysis (tools/wave_trace.py)
   const char* trace_path = std::getenv("RTG_WAVE_TRACE");
   int64_t trace_slots = 0;
   if (trace_path) {
-    trace_slots = variant == 3 ? int64_t(grid_blocks) * kLdsWaves
-                               : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
+    trace_slots = variant == 3 || variant == 0 ? int64_t(grid_waves)
+                                               : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
     RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.trace), trace_slots * 32, stream), "hipMalloc(trace)");
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
   }
@@ -785,7 +818,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     dj.chunk_samples = std::max(1, cam->samples_per_pixel);
   }
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
-  RTG_HIP(launch_render(s->dev, dc, dj, s->info.stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
+  RTG_HIP(launch_render(s->dev, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
                         variant, lds_bytes, grid_blocks, stream),
           "render kernel launch");
   if (chunked)
@@ -793,6 +826,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
             "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
   if (chunked) RTG_HIP(hipFreeAsync(dj.partial, stream), "hipFreeAsync(partial sums)");
+  if (dj.spill) RTG_HIP(hipFreeAsync(dj.spill, stream), "hipFreeAsync(stack spill)");
   if (trace_path) {
     std::vector<unsigned long long> tr(static_cast<size_t>(trace_slots) * 4);
     RTG_HIP(hipMemcpyAsync(tr.data(), dj.trace, trace_slots * 32, hipMemcpyDeviceToHost, stream), "trace copy");

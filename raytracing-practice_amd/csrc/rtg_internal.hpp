@@ -125,6 +125,8 @@ struct DevScene {
   int32_t num_perlins;  // perlin tables (256 gradients + 3 x 256 permutations each)
 };
 
+constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
+
 struct DevJob {
   uint64_t seed_mix;
   int32_t row_begin;
@@ -141,6 +143,9 @@ struct DevJob {
   int32_t chunks;         // sample chunks per pixel (work units = pixel x chunk), >= 1
   int32_t chunk_samples;  // K: samples per chunk (the last chunk may be shorter)
   float* partial;         // chunks > 1: [chunk][row][column][3] partial sums; else null
+  int32_t* spill;         // traversal-stack entries beyond the LDS part: [wave][depth][lane]
+  int32_t spill_depth;    // entries per lane in `spill` (0: the LDS stack suffices)
+  int32_t lds_stack;      // stack entries kept in LDS (the kernel's STACK; tests may lower it)
   // optional per-wave timeline (RTG_WAVE_TRACE, tools/wave_trace.py): 4 x u64 per wave =
   // {s_memrealtime at start, at end, pixels finished, block << 8 | wave}; null when off
   unsigned long long* trace;

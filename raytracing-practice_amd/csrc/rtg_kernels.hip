@@ -183,19 +183,54 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.active = S.num_nodes > 0;
 }
 
-__device__ __forceinline__ void trav_pop(Trav& t, int32_t* stk) {
+// Per-lane traversal stacks, laid out [depth][lane] (bank-conflict-free ds_read/write_b32).
+// LdsStack: all N entries in LDS. SpillStack: the first N entries in LDS, deeper ones (deep BVHs
+// only, e.g. the 1M-sphere scene's 36-entry bound) in a global per-wave area of the same layout,
+// so the LDS part stays small enough for full occupancy and no tree is too deep.
+template <int N>
+struct LdsStack {
+  int32_t* lds;
+  __device__ __forceinline__ int32_t capacity() const { return N; }
+  __device__ __forceinline__ void store(int32_t sp, int32_t v) const { lds[sp * 64] = v; }
+  __device__ __forceinline__ int32_t load(int32_t sp) const { return lds[sp * 64]; }
+};
+template <int N>
+struct SpillStack {
+  int32_t* lds;
+  int32_t* spill;  // this lane's global area, entries n.. at spill[(sp - n) * 64]
+  int32_t n;       // entries kept in LDS (<= N; J.lds_stack, lowered only by tests)
+  int32_t cap;     // n + spill depth
+  __device__ __forceinline__ int32_t capacity() const { return cap; }
+  __device__ __forceinline__ void store(int32_t sp, int32_t v) const {
+    if (__builtin_expect(sp < n, 1))
+      lds[sp * 64] = v;
+    else
+      spill[(sp - n) * 64] = v;
+  }
+  __device__ __forceinline__ int32_t load(int32_t sp) const {
+    int32_t v;
+    if (__builtin_expect(sp < n, 1))
+      v = lds[sp * 64];
+    else
+      v = spill[(sp - n) * 64];
+    return v;
+  }
+};
+
+template <class Stk>
+__device__ __forceinline__ void trav_pop(Trav& t, const Stk& stk) {
   if (t.sp == 0) {
     t.active = false;
     return;
   }
   --t.sp;
-  t.todo = stk[t.sp * 64];
+  t.todo = stk.load(t.sp);
 }
 
 // Visit one inner node (t.todo >= 0): test both child boxes, continue with the nearer hit child
 // and push the farther one, or pop when neither is hit.
-template <int STACK, bool COUNT>
-__device__ __forceinline__ void node_step(Trav& t, const DevScene& S, int32_t* stk, Counts<COUNT>& cnt,
+template <class Stk, bool COUNT>
+__device__ __forceinline__ void node_step(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                           bool& overflow, bool& corrupt) {
   if (t.todo >= S.num_nodes) {  // corrupt child code: report, never read out of bounds
     corrupt = true;
@@ -225,8 +260,8 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, int32_t* s
   const bool hr = rn <= rf && ch.y != kEmptyChild;
   if (hl && hr) {
     const bool lfirst = ln <= rn;
-    if (t.sp < STACK) {
-      stk[t.sp * 64] = lfirst ? ch.y : ch.x;
+    if (t.sp < stk.capacity()) {
+      stk.store(t.sp, lfirst ? ch.y : ch.x);
       ++t.sp;
     } else {
       overflow = true;
@@ -266,8 +301,8 @@ __device__ __forceinline__ void usort(uint32_t& a, uint32_t& b) {
 // far-to-near. Empty slots hold the inverted box (+inf, -inf): whatever the signs, at least one
 // axis has a finite 1/d, for which the near plane gives tn = +inf and the far one tf = -inf, so an
 // empty slot can never be entered (rays with all three components zero do not exist).
-template <int STACK, bool COUNT>
-__device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* stk, Counts<COUNT>& cnt,
+template <class Stk, bool COUNT>
+__device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
   // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
   if (t.todo >= S.num_nodes * 112) {
@@ -310,20 +345,20 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, int32_t* 
   const char* codes = nb + 96;
   auto code_of = [&](uint32_t k) { return *reinterpret_cast<const int32_t*>(codes + (k & 12u)); };
   const int npush = (k1 != ~0u) + (k2 != ~0u) + (k3 != ~0u);
-  if (t.sp + npush > STACK) {
+  if (t.sp + npush > stk.capacity()) {
     overflow = true;
   } else {
-    if (k3 != ~0u) stk[(t.sp++) * 64] = code_of(k3);
-    if (k2 != ~0u) stk[(t.sp++) * 64] = code_of(k2);
-    if (k1 != ~0u) stk[(t.sp++) * 64] = code_of(k1);
+    if (k3 != ~0u) stk.store(t.sp++, code_of(k3));
+    if (k2 != ~0u) stk.store(t.sp++, code_of(k2));
+    if (k1 != ~0u) stk.store(t.sp++, code_of(k1));
   }
   t.todo = code_of(k0);
 }
 
 // Test the primitives of one leaf (t.todo < 0), then pop.
-template <bool COUNT>
+template <class Stk, bool COUNT>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
-                                          int32_t* stk, Counts<COUNT>& cnt, bool& corrupt) {
+                                          const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
   const int32_t code = ~t.todo;
   const int32_t first = code >> 3;
   const int32_t count = (code & 7) + 1;
@@ -364,14 +399,14 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
 }
 
 // One unit of traversal work for this lane (used by the per-segment schedule).
-template <int STACK, bool COUNT>
+template <class Stk, bool COUNT>
 __device__ __forceinline__ void trav_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
-                                          int32_t* stk, Counts<COUNT>& cnt, bool& overflow,
+                                          const Stk& stk, Counts<COUNT>& cnt, bool& overflow,
                                           bool& corrupt) {
   if (t.todo >= 0)
-    node_step<STACK, COUNT>(t, S, stk, cnt, overflow, corrupt);
+    node_step<Stk, COUNT>(t, S, stk, cnt, overflow, corrupt);
   else
-    leaf_step<COUNT>(t, S, o, d, time, stk, cnt, corrupt);
+    leaf_step<Stk, COUNT>(t, S, o, d, time, stk, cnt, corrupt);
 }
 
 // Schedule 2: the first kernel's monolithic closest-hit loop (kept for A/B).
@@ -793,9 +828,9 @@ __device__ __forceinline__ void start_pixel_sample(PathState& ps, const DevCamer
 // or a leaf step for the whole wave (leaf work waits until leaf_batch lanes have reached a leaf);
 // the wave switches to shading once ceil(alive * shade_batch / 64) lanes have finished their
 // closest-hit query, and lanes still traversing keep their stack and continue afterwards.
-template <int STACK, bool COUNT, int WIDE, bool TEXF>
+template <class Stk, bool COUNT, int WIDE, bool TEXF>
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                              int32_t* stk, WaveStats<COUNT>& w) {
+                                              const Stk& stk, WaveStats<COUNT>& w) {
   const int lane = __lane_id();
   const bool no_work = C.max_depth <= 0 || C.spp <= 0;  // every pixel is black (camera.hpp:192)
   const int num_batches = J.num_tiles * J.chunks;
@@ -882,14 +917,14 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       if (leaf_trip && tr.active && tr.todo < 0)
-        leaf_step<COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+        leaf_step<Stk, COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       if (tr.active && tr.todo >= 0) {
         if constexpr (WIDE == 4)
-          node_step4<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+          node_step4<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
         else
-          node_step<STACK, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+          node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
       }
       if (COUNT && leaf_trip) w.diag[8] += __builtin_amdgcn_s_memtime() - tl;
       const uint64_t trav = __ballot(tr.active);
@@ -955,18 +990,24 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
 
 // Schedule 4: the same loop on a plain grid of 256-thread workgroups (scene read through the
 // caches; used when it does not fit in LDS). Waves take tiles from the same counter.
-template <int STACK, bool COUNT, int WIDE, bool TEXF>
+template <int STACK, bool SPILL, bool COUNT, int WIDE, bool TEXF>
 __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
   __shared__ int32_t s_stack[4 * STACK * 64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  int32_t* stk = s_stack + wave * STACK * 64 + lane;
+  const int slot = blockIdx.x * 4 + wave;
+  int32_t* lstk = s_stack + wave * STACK * 64 + lane;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   WaveStats<COUNT> w;
-  render_stream<STACK, COUNT, WIDE, TEXF>(S, C, J, stk, w);
+  if constexpr (SPILL) {
+    const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
+                                J.lds_stack, J.lds_stack + J.spill_depth};
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF>(S, C, J, stk, w);
+  } else {
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF>(S, C, J, LdsStack<STACK>{lstk}, w);
+  }
   flush_stats<COUNT>(J, w, lane);
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-  trace_wave(J, t0, w.pixels, lane, blk * 4 + wave, (blk << 8) | wave);
+  trace_wave(J, t0, w.pixels, lane, slot, (blockIdx.x << 8) | wave);
 }
 
 // Schedule 3 (default when the geometry fits): persistent workgroups of WAVES waves, one per CU.
@@ -974,13 +1015,13 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
 // L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
 // left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
-template <int STACK, bool COUNT, int WAVES, int WIDE, bool TEXF>
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF>
 __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  int32_t* stk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
+  int32_t* lstk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
   float4* l_nodes = reinterpret_cast<float4*>(smem + J.lds_nodes);
   int32_t* l_refs = reinterpret_cast<int32_t*>(smem + J.lds_refs);
   float4* l_spheres = reinterpret_cast<float4*>(smem + J.lds_spheres);
@@ -1013,7 +1054,14 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
     L.perlin_perm = l_pperm;
   }
   WaveStats<COUNT> w;
-  render_stream<STACK, COUNT, WIDE, TEXF>(L, C, J, stk, w);
+  if constexpr (SPILL) {
+    const int slot = blockIdx.x * WAVES + wave;
+    const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
+                                J.lds_stack, J.lds_stack + J.spill_depth};
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF>(L, C, J, stk, w);
+  } else {
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF>(L, C, J, LdsStack<STACK>{lstk}, w);
+  }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, blockIdx.x * WAVES + wave, (blockIdx.x << 8) | wave);
 }
@@ -1039,7 +1087,8 @@ __global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCame
   while (sample < C.spp) {
     Trav tr;
     trav_begin(tr, S, ps.o, ps.d);
-    while (tr.active) trav_step<STACK, COUNT>(tr, S, ps.o, ps.d, ps.time, stk, cnt, overflow, corrupt);
+    while (tr.active)
+      trav_step<LdsStack<STACK>, COUNT>(tr, S, ps.o, ps.d, ps.time, LdsStack<STACK>{stk}, cnt, overflow, corrupt);
     ++segs;
     bool alive;
     if (tr.best < 0) {
@@ -1153,52 +1202,63 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
-template <int STACK, int WIDE, bool TEXF>
+template <int STACK, bool SPILL, int WIDE, bool TEXF>
 hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                       int lds_bytes, int grid_blocks, hipStream_t stream) {
-  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, true, kLdsWaves, WIDE, TEXF>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, false, kLdsWaves, WIDE, TEXF>);
+  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (count)
-    hipLaunchKernelGGL((render_kernel_lds<STACK, true, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
+    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
                        dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel_lds<STACK, false, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
+    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
                        dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   return hipGetLastError();
 }
 
-template <int STACK, int WIDE, bool TEXF>
-hipError_t launch_plain(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
+template <int STACK, bool SPILL, int WIDE, bool TEXF>
+hipError_t launch_plain(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int grid_blocks,
                         hipStream_t stream) {
-  const dim3 block(256);
-  const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
   if (count)
-    hipLaunchKernelGGL((render_kernel<STACK, true, WIDE, TEXF>), grid, block, 0, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel<STACK, SPILL, true, WIDE, TEXF>), dim3(grid_blocks), dim3(256), 0, stream,
+                       S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel<STACK, false, WIDE, TEXF>), grid, block, 0, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel<STACK, SPILL, false, WIDE, TEXF>), dim3(grid_blocks), dim3(256), 0, stream,
+                       S, C, J);
   return hipGetLastError();
 }
 
-template <int STACK, int WIDE>
-hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
+// The default schedules: persistent LDS kernel (16 LDS stack entries) or the plain grid (16, or 32
+// with a global spill for deeper trees), each with / without the image-and-noise texture paths.
+template <int WIDE>
+hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int stack,
                           bool lds, int lds_bytes, int grid_blocks, hipStream_t stream) {
-  if (lds)
-    return S.tex_full ? launch_lds<STACK, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
-                      : launch_lds<STACK, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
-  return S.tex_full ? launch_plain<STACK, WIDE, true>(S, C, J, count, stream)
-                    : launch_plain<STACK, WIDE, false>(S, C, J, count, stream);
+  const bool spill = J.spill_depth > 0;
+  const bool tex = S.tex_full != 0;
+  if (lds) {
+    if (stack != kLdsStack || J.lds_stack > kLdsStack) return hipErrorInvalidValue;
+    if (spill)
+      return tex ? launch_lds<kLdsStack, true, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
+                 : launch_lds<kLdsStack, true, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+    return tex ? launch_lds<kLdsStack, false, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
+               : launch_lds<kLdsStack, false, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+  }
+  if (stack > 32 || J.lds_stack > stack) return hipErrorInvalidValue;
+  if (spill)  // (any LDS part <= 32 entries, J.lds_stack, plus the global spill)
+    return tex ? launch_plain<32, true, WIDE, true>(S, C, J, count, grid_blocks, stream)
+               : launch_plain<32, true, WIDE, false>(S, C, J, count, grid_blocks, stream);
+  if (stack == 16)
+    return tex ? launch_plain<16, false, WIDE, true>(S, C, J, count, grid_blocks, stream)
+               : launch_plain<16, false, WIDE, false>(S, C, J, count, grid_blocks, stream);
+  return tex ? launch_plain<32, false, WIDE, true>(S, C, J, count, grid_blocks, stream)
+             : launch_plain<32, false, WIDE, false>(S, C, J, count, grid_blocks, stream);
 }
 
 template <int STACK>
-hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
-                        int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
-  const bool wide = S.node_width == 4;
-  if (variant == 3 || variant == 0)
-    return wide ? launch_default<STACK, 4>(S, C, J, count, variant == 3, lds_bytes, grid_blocks, stream)
-                : launch_default<STACK, 2>(S, C, J, count, variant == 3, lds_bytes, grid_blocks, stream);
-  if (wide) return hipErrorInvalidValue;  // schedules 1 and 2 traverse binary nodes only
+hipError_t launch_legacy(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int variant,
+                         hipStream_t stream) {
   const dim3 block(256);
   const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
   if (variant == 2) {
@@ -1206,7 +1266,7 @@ hipError_t launch_stack(const DevScene& S, const DevCamera& C, const DevJob& J, 
       hipLaunchKernelGGL((render_kernel_v0<STACK, true>), grid, block, 0, stream, S, C, J);
     else
       hipLaunchKernelGGL((render_kernel_v0<STACK, false>), grid, block, 0, stream, S, C, J);
-  } else if (variant == 1) {
+  } else {
     if (count)
       hipLaunchKernelGGL((render_kernel_segment<STACK, true>), grid, block, 0, stream, S, C, J);
     else
@@ -1262,13 +1322,17 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
                          bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
   if (J.row_count <= 0 || C.width <= 0) return hipSuccess;
+  if (variant == 3 || variant == 0)
+    return S.node_width == 4 ? launch_default<4>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream)
+                             : launch_default<2>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream);
+  if (S.node_width != 2) return hipErrorInvalidValue;  // schedules 1 and 2 traverse binary nodes only
   switch (stack) {
     case 16:
-      return launch_stack<16>(S, C, J, count, variant, lds_bytes, grid_blocks, stream);
+      return launch_legacy<16>(S, C, J, count, variant, stream);
     case 32:
-      return launch_stack<32>(S, C, J, count, variant, lds_bytes, grid_blocks, stream);
+      return launch_legacy<32>(S, C, J, count, variant, stream);
     case 64:
-      return launch_stack<64>(S, C, J, count, variant, lds_bytes, grid_blocks, stream);
+      return launch_legacy<64>(S, C, J, count, variant, stream);
     default:
       return hipErrorInvalidValue;
   }

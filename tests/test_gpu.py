@@ -213,6 +213,31 @@ def test_empty_world_and_single_sphere(gpu_lib, oracle):
     assert_parity(g, o, st, segs)
 
 
+def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypatch):
+    """Deep BVHs keep the first stack entries in LDS and the rest in a global per-wave spill area
+    (the 1M-sphere scene needs 36 entries). RTG_STACK_LDS_ENTRIES lowers the LDS part so that the
+    spill path carries most of the stack here: both default schedules must still match the oracle
+    bit for bit."""
+    import ctypes as C
+
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 96, 4, 20
+    ds = gpu_lib.scene_create(s.desc)
+    o, segs = oracle.render_f32(s.desc, c)
+    H = gpu_lib.camera_resolve(c).image_height
+    for entries in ("1", "3"):
+        monkeypatch.setenv("RTG_STACK_LDS_ENTRIES", entries)
+        for flags in (0, rtgpu.RTG_RENDER_SCHEDULE(4)):
+            out = np.zeros((H, 96, 3), dtype=np.float32)
+            job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, 0, 1, 0, flags, None)
+            st = rtgpu.rtg_render_stats()
+            gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job),
+                                                                out.ctypes.data, C.byref(st)))
+            assert_parity(out, o, st, segs)
+    ds.close()
+
+
 def test_million_sphere_scene(gpu_lib, scenes, oracle):
     """BASELINE config 5 scene (grid 500 -> 1,000,001 objects, deep BVH) at a small image."""
     g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", grid=500, image_width=64,

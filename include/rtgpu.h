@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 2
+#define RTG_ABI_VERSION 3
 
 typedef int32_t rtg_status;
 #define RTG_OK 0
@@ -171,6 +171,11 @@ static inline int rtg_chunk_samples(int spp) {
   return spp > 0 ? (spp + n - 1) / n : 1;
 }
 
+static inline int rtg_num_chunks(int spp) {
+  int k = rtg_chunk_samples(spp);
+  return spp > 0 ? (spp + k - 1) / k : 1;
+}
+
 typedef struct rtg_render_desc {
   uint64_t seed;      /* run seed of the counter RNG */
   int32_t row_begin;  /* first image row of this shard */
@@ -178,6 +183,16 @@ typedef struct rtg_render_desc {
   int32_t row_count;  /* <= 0: every row reachable from row_begin with row_stride */
   int32_t flags;      /* RTG_RENDER_* */
   void* stream;       /* hipStream_t to launch on; NULL = the library's own stream */
+  /* Progressive / checkpointable rendering. NULL partial: one-shot render (fields below unused).
+   * Otherwise `partial` is a DEVICE buffer of rtg_num_chunks(spp) x rows x width x 3 floats holding
+   * per-chunk partial sums (layout [chunk][row][column][rgb]); only chunks [chunk_begin,
+   * chunk_begin + chunk_count) are rendered into it (chunk_count <= 0: through the last chunk),
+   * the rest of the buffer is left alone, and out_rgb (may be NULL) receives the mean over the
+   * samples of chunks [0, chunk_begin + chunk_count). Once every chunk has been rendered the
+   * mean is bit-identical to a one-shot render; saving the buffer is a checkpoint. */
+  float* partial;
+  int32_t chunk_begin;
+  int32_t chunk_count;
 } rtg_render_desc;
 
 typedef struct rtg_render_stats {

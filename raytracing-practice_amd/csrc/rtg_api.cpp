@@ -697,7 +697,9 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
 
 rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,
                       float* out_rgb, rtg_render_stats* stats) {
-  if (!s || !cam || !job || !out_rgb) return fail(RTG_E_INVALID, "null argument");
+  if (!s || !cam || !job) return fail(RTG_E_INVALID, "null argument");
+  const bool progressive = job->partial != nullptr;
+  if (!out_rgb && !progressive) return fail(RTG_E_INVALID, "null output buffer");
   if (cam->image_width <= 0 || cam->samples_per_pixel <= 0)
     return fail(RTG_E_INVALID, "image_width and samples_per_pixel must be positive");
   if (job->row_stride <= 0 || job->row_begin < 0) return fail(RTG_E_INVALID, "bad row range");
@@ -739,7 +741,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   hipStream_t stream = job->stream ? static_cast<hipStream_t>(job->stream) : s->own_stream;
   const size_t out_bytes = static_cast<size_t>(rows) * W * 3 * sizeof(float);
   float* dout = out_rgb;
-  if (!dev_out) {
+  if (!dev_out && out_rgb) {
     RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dout), out_bytes, stream), "hipMallocAsync(out)");
   }
   DevJob dj{};
@@ -757,8 +759,26 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dj.chunk_samples = rtg_chunk_samples(cam->samples_per_pixel);
   // RTG_CHUNK_SAMPLES overrides K for schedule experiments (the frame then differs from the spec)
   if (const char* e = std::getenv("RTG_CHUNK_SAMPLES")) dj.chunk_samples = std::max(1, std::atoi(e));
-  dj.chunks = cam->samples_per_pixel > 0 ? (cam->samples_per_pixel + dj.chunk_samples - 1) / dj.chunk_samples : 1;
+  const int total_chunks =
+      cam->samples_per_pixel > 0 ? (cam->samples_per_pixel + dj.chunk_samples - 1) / dj.chunk_samples : 1;
+  dj.chunks = total_chunks;
+  dj.chunk_begin = 0;
   dj.partial = nullptr;
+  int sum_chunks = total_chunks;  // chunks the output mean covers
+  float out_scale = dc.scale;
+  if (progressive) {
+    if (job->chunk_begin < 0 || job->chunk_begin >= total_chunks)
+      return fail(RTG_E_INVALID, "chunk_begin outside [0, rtg_num_chunks(spp))");
+    dj.chunk_begin = job->chunk_begin;
+    dj.chunks = job->chunk_count <= 0 ? total_chunks - job->chunk_begin
+                                      : std::min(job->chunk_count, total_chunks - job->chunk_begin);
+    dj.partial = job->partial;
+    sum_chunks = dj.chunk_begin + dj.chunks;
+    const int samples_done = std::min(cam->samples_per_pixel, sum_chunks * dj.chunk_samples);
+    // the final mean uses pixel_samples_scale itself (H7), so a finished progressive render is
+    // bit-identical to a one-shot one
+    out_scale = sum_chunks == total_chunks ? dc.scale : 1.0f / static_cast<float>(samples_done);
+  }
 
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
@@ -809,7 +829,9 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.trace), trace_slots * 32, stream), "hipMalloc(trace)");
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
   }
-  const bool chunked = dj.chunks > 1 && (variant == 3 || variant == 0) && dc.max_depth > 0;
+  if (progressive && !(variant == 3 || variant == 0))
+    return fail(RTG_E_INVALID, "progressive rendering needs the default schedules");
+  const bool chunked = !progressive && dj.chunks > 1 && (variant == 3 || variant == 0) && dc.max_depth > 0;
   if (chunked)
     RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.partial), out_bytes * dj.chunks, stream),
             "hipMallocAsync(partial sums)");
@@ -817,12 +839,18 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     dj.chunks = 1;
     dj.chunk_samples = std::max(1, cam->samples_per_pixel);
   }
+  const bool skip_kernel = progressive && dc.max_depth <= 0;  // every chunk sum is black
+  if (skip_kernel)
+    RTG_HIP(hipMemsetAsync(dj.partial + static_cast<size_t>(dj.chunk_begin) * rows * W * 3, 0,
+                           out_bytes * dj.chunks, stream),
+            "hipMemsetAsync(partial sums)");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
-  RTG_HIP(launch_render(s->dev, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
-                        variant, lds_bytes, grid_blocks, stream),
-          "render kernel launch");
-  if (chunked)
-    RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, dj.chunks, dc.scale, stream),
+  if (!skip_kernel)
+    RTG_HIP(launch_render(s->dev, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
+                          variant, lds_bytes, grid_blocks, stream),
+            "render kernel launch");
+  if (chunked || (progressive && dout))
+    RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, sum_chunks, out_scale, stream),
             "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
   if (chunked) RTG_HIP(hipFreeAsync(dj.partial, stream), "hipFreeAsync(partial sums)");
@@ -840,13 +868,18 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   RTG_HIP(hipMemcpyAsync(s->host_counters, s->counters, kNumCounters * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, stream),
           "hipMemcpyAsync(counters)");
-  if (!dev_out) {
+  if (!dev_out && out_rgb) {
     RTG_HIP(hipMemcpyAsync(out_rgb, dout, out_bytes, hipMemcpyDeviceToHost, stream), "hipMemcpy(out)");
     RTG_HIP(hipFreeAsync(dout, stream), "hipFreeAsync(out)");
   }
   s->pending = true;
   s->pending_stream = stream;
-  s->pending_samples = static_cast<uint64_t>(rows) * W * cam->samples_per_pixel;
+  {
+    const int s0 = std::min(cam->samples_per_pixel, dj.chunk_begin * dj.chunk_samples);
+    const int s1 = progressive ? std::min(cam->samples_per_pixel, (dj.chunk_begin + dj.chunks) * dj.chunk_samples)
+                               : cam->samples_per_pixel;
+    s->pending_samples = static_cast<uint64_t>(rows) * W * static_cast<uint64_t>(s1 - s0);
+  }
   if (async) return RTG_OK;
   return collect_stats(s, stats);
 }

@@ -140,7 +140,9 @@ struct DevJob {
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 8x8 pixel tiles per shard row of tiles
   int32_t num_tiles;  // 8x8 pixel tiles in the shard; work is handed out in 4x4 quarters of them
-  int32_t chunks;         // sample chunks per pixel (work units = pixel x chunk), >= 1
+  int32_t chunks;         // sample chunks rendered by this launch (work units = pixel x chunk)
+  int32_t chunk_begin;    // first of them (progressive rendering; 0 for a one-shot frame)
+  int32_t pad4_;
   int32_t chunk_samples;  // K: samples per chunk (the last chunk may be shorter)
   float* partial;         // chunks > 1: [chunk][row][column][3] partial sums; else null
   int32_t* spill;         // traversal-stack entries beyond the LDS part: [wave][depth][lane]

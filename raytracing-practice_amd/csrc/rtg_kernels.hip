@@ -897,7 +897,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           break;
         }
         const int tile = b / J.chunks;
-        bc = b - tile * J.chunks;
+        bc = J.chunk_begin + (b - tile * J.chunks);
         const int ty = tile / J.tiles_x;
         bx = (tile - ty * J.tiles_x) * 8;
         by = ty * 8;

@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 
-RTG_ABI_VERSION = 2
+RTG_ABI_VERSION = 3
 RTG_OK = 0
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
 RTG_MAT_LAMBERTIAN, RTG_MAT_METAL, RTG_MAT_DIELECTRIC, RTG_MAT_DIFFUSE_LIGHT = 1, 2, 3, 4
@@ -93,7 +93,8 @@ class rtg_camera_params(C.Structure):
 
 class rtg_render_desc(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("row_begin", C.c_int32), ("row_stride", C.c_int32),
-                ("row_count", C.c_int32), ("flags", C.c_int32), ("stream", C.c_void_p)]
+                ("row_count", C.c_int32), ("flags", C.c_int32), ("stream", C.c_void_p),
+                ("partial", C.c_void_p), ("chunk_begin", C.c_int32), ("chunk_count", C.c_int32)]
 
 
 class rtg_render_stats(C.Structure):
@@ -139,6 +140,12 @@ def chunk_samples(spp: int) -> int:
     """rtgpu.h rtg_chunk_samples: samples per accumulation chunk of the rtg-f32 spec."""
     n = max(1, (spp + 63) // 64)
     return (spp + n - 1) // n if spp > 0 else 1
+
+
+def num_chunks(spp: int) -> int:
+    """rtgpu.h rtg_num_chunks: accumulation chunks of a pixel (progressive-rendering units)."""
+    k = chunk_samples(spp)
+    return (spp + k - 1) // k if spp > 0 else 1
 
 
 class Library:
@@ -253,6 +260,23 @@ class DeviceScene:
         st = rtg_render_stats()
         self.L.check("rtg_render", self.L.lib.rtg_render(self.handle, C.byref(cam), C.byref(job),
                                                           C.c_void_p(out_ptr), C.byref(st)))
+        return st
+
+    def render_chunks(self, cam: rtg_camera_desc, partial_ptr: int, chunk_begin: int, chunk_count: int,
+                      out_ptr: int = 0, stream_ptr: Optional[int] = None, seed: int = DEFAULT_SEED,
+                      row_begin: int = 0, row_stride: int = 1, row_count: int = 0) -> rtg_render_stats:
+        """Progressive rendering (rtgpu.h rtg_render_desc.partial): render sample chunks
+        [chunk_begin, chunk_begin + chunk_count) into the device partial-sum buffer at partial_ptr
+        (num_chunks(spp) x rows x W x 3 float32) and, when out_ptr is given, write the running mean
+        of chunks [0, chunk_begin + chunk_count) there (device memory)."""
+        flags = RTG_RENDER_OUT_DEVICE
+        job = rtg_render_desc(seed, row_begin, row_stride, row_count, flags,
+                              C.c_void_p(stream_ptr) if stream_ptr else None,
+                              C.c_void_p(partial_ptr), chunk_begin, chunk_count)
+        st = rtg_render_stats()
+        self.L.check("rtg_render", self.L.lib.rtg_render(self.handle, C.byref(cam), C.byref(job),
+                                                          C.c_void_p(out_ptr) if out_ptr else None,
+                                                          C.byref(st)))
         return st
 
     def wait(self) -> rtg_render_stats:

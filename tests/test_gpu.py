@@ -154,6 +154,42 @@ def test_sample_chunks_match_oracle(gpu_lib, scenes, oracle, spp):
     assert np.array_equal(g, gs)  # deterministic whatever order the units ran in
 
 
+def test_progressive_chunks_and_checkpoint(gpu_lib, scenes):
+    """Progressive rendering (rtg_render_desc.partial): chunks rendered in several calls, with a
+    checkpoint (partial sums copied to the host, the scene destroyed and rebuilt) in between,
+    reproduce the one-shot frame bit for bit; the running mean uses the samples done so far."""
+    import torch
+
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 80, 200, 20
+    n = rtgpu.num_chunks(200)
+    K = rtgpu.chunk_samples(200)
+    assert (n, K) == (4, 50)
+    ds = gpu_lib.scene_create(s.desc)
+    full, _ = ds.render_host(c, seed=7)
+    H = full.shape[0]
+    stream = torch.cuda.current_stream().cuda_stream
+    partial = torch.zeros((n, H, 80, 3), dtype=torch.float32, device="cuda")
+    out = torch.zeros((H, 80, 3), dtype=torch.float32, device="cuda")
+    st = ds.render_chunks(c, partial.data_ptr(), 0, 1, out.data_ptr(), stream, seed=7)
+    torch.cuda.synchronize()
+    assert st.samples == H * 80 * K
+    first = partial[0].cpu().numpy()
+    assert np.array_equal(out.cpu().numpy(), np.float32(1.0 / K) * first)
+    ds.render_chunks(c, partial.data_ptr(), 1, 2, 0, stream, seed=7)
+    torch.cuda.synchronize()
+    saved = partial.cpu()  # checkpoint
+    ds.close()
+    ds = gpu_lib.scene_create(s.desc)
+    resumed = saved.cuda()
+    ds.render_chunks(c, resumed.data_ptr(), 3, 0, out.data_ptr(), stream, seed=7)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), full)
+    assert np.array_equal(resumed[:3].cpu().numpy(), saved[:3].numpy())  # finished chunks untouched
+    ds.close()
+
+
 @pytest.mark.parametrize("case", ["one_pixel", "odd_width", "depth0", "depth1", "spp1", "pinhole",
                                   "tall"])
 def test_edge_cases(gpu_lib, scenes, oracle, case):

@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
-    ap.add_argument("--bvh", choices=["sah", "median"], default="sah")
+    ap.add_argument("--bvh", choices=["sah", "median", "gpu"], default="sah")
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=None,
@@ -129,7 +129,7 @@ def main():
 
     lib = rtgpu.Library()
     scenes = rtgpu.SceneLibrary()
-    bvh = rtgpu.RTG_BVH_SAH if args.bvh == "sah" else rtgpu.RTG_BVH_MEDIAN
+    bvh = {"sah": rtgpu.RTG_BVH_SAH, "median": rtgpu.RTG_BVH_MEDIAN, "gpu": rtgpu.RTG_BVH_GPU}[args.bvh]
     t0 = time.perf_counter()
     s = scenes.build(args.scene, grid=args.grid, image_width=args.width,
                      aspect_ratio=args.width / args.height, spp=args.spp, max_depth=args.depth,

@@ -101,6 +101,8 @@ typedef struct rtg_perlin {
 /* BVH construction modes (the library always builds its own device BVH). */
 #define RTG_BVH_MEDIAN 0 /* bvh_node.hpp:25-77: longest axis, std::sort by bbox.min, median */
 #define RTG_BVH_SAH 1    /* binned SAH, leaves of <= 4 primitives, collapsed to 4-wide nodes */
+#define RTG_BVH_GPU 3    /* built on the device: Morton-code LBVH (Karras) collapsed to 4-wide nodes;
+                            milliseconds for 1M primitives, more traversal steps than SAH */
 
 typedef struct rtg_scene_desc {
   uint32_t abi_version; /* RTG_ABI_VERSION */

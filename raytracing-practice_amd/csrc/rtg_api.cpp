@@ -217,15 +217,32 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   rtg_scene_desc bd = *d;
   const bool binary_sah = d->bvh_mode == 2;
   if (binary_sah) bd.bvh_mode = RTG_BVH_SAH;
+  const bool gpu_bvh = d->bvh_mode == RTG_BVH_GPU;
   Bvh bvh;
-  if (!build_bvh(&bd, &bvh, err)) return false;
+  if (gpu_bvh) {  // primitives in input order; the device builds the tree (rtg_gpubvh.hip)
+    if (d->num_prims > (int64_t(1) << 28) || d->num_prims > INT32_MAX / 112) {
+      *err = "too many primitives for the device BVH builder";
+      return false;
+    }
+    bvh.refs.resize(d->num_prims);
+    for (int64_t i = 0; i < d->num_prims; ++i) bvh.refs[i] = i;
+  } else if (!build_bvh(&bd, &bvh, err)) {
+    return false;
+  }
   out->num_prims = d->num_prims;
   out->num_nodes = static_cast<int64_t>(bvh.nodes.size());
   out->depth = bvh.depth;
   out->stack_need = bvh.depth;
   out->node_width = 2;
   Bvh4 bvh4;
-  if (d->bvh_mode == RTG_BVH_SAH && !bvh.nodes.empty()) {
+  if (gpu_bvh) {
+    out->gpu_bvh = true;
+    out->node_width = 4;
+    out->node_capacity = std::max<int64_t>(1, d->num_prims);
+    out->num_nodes = 0;
+    out->depth = 0;
+    out->stack_need = 0;
+  } else if (d->bvh_mode == RTG_BVH_SAH && !bvh.nodes.empty()) {
     collapse_bvh4(bvh, &bvh4);
     out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
     out->depth = bvh4.depth;
@@ -559,7 +576,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     size_t off;
   };
   Part parts[9] = {
-      {hs.nodes.data(), hs.nodes.size() * 4, 0},       {hs.refs.data(), hs.refs.size() * 4, 0},
+      {hs.gpu_bvh ? nullptr : hs.nodes.data(),
+       hs.gpu_bvh ? static_cast<size_t>(hs.node_capacity) * 112 : hs.nodes.size() * 4, 0},       {hs.refs.data(), hs.refs.size() * 4, 0},
       {hs.spheres.data(), hs.spheres.size() * 4, 0},   {hs.quads.data(), hs.quads.size() * 4, 0},
       {hs.materials.data(), hs.materials.size() * 4, 0}, {hs.textures.data(), hs.textures.size() * 4, 0},
       {hs.image_hdr.data(), hs.image_hdr.size() * 4, 0}, {hs.texels.data(), hs.texels.size(), 0},
@@ -593,7 +611,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     return cleanup(hip_fail(e, "hipHostMalloc(counters)"));
   char* base = static_cast<char*>(s->dmem);
   for (const Part& p : parts) {
-    if (p.bytes == 0) continue;
+    if (p.bytes == 0 || !p.src) continue;
     if ((e = hipMemcpyAsync(base + p.off, p.src, p.bytes, hipMemcpyHostToDevice, s->own_stream)) !=
         hipSuccess)
       return cleanup(hip_fail(e, "hipMemcpy(scene)"));
@@ -605,6 +623,27 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   if ((e = hipStreamSynchronize(s->own_stream)) != hipSuccess)
     return cleanup(hip_fail(e, "hipStreamSynchronize(upload)"));
   const auto t2 = std::chrono::steady_clock::now();
+  double gpu_build_ms = 0.0;
+  if (hs.gpu_bvh && hs.num_prims > 0) {  // RTG_BVH_GPU: build the nodes and leaf-ordered refs here
+    int32_t* refs_dev = reinterpret_cast<int32_t*>(base + parts[1].off);
+    int32_t* sorted = nullptr;
+    if ((e = hipMallocAsync(reinterpret_cast<void**>(&sorted), hs.num_prims * 4, s->own_stream)) != hipSuccess)
+      return cleanup(hip_fail(e, "hipMalloc(bvh refs)"));
+    GpuBvhResult r{};
+    e = gpu_build_bvh4(reinterpret_cast<const float4*>(base + parts[2].off),
+                       reinterpret_cast<const float4*>(base + parts[3].off), refs_dev, hs.num_prims,
+                       reinterpret_cast<float*>(base + parts[0].off), hs.node_capacity, sorted, &r, s->own_stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(refs_dev, sorted, hs.num_prims * 4, hipMemcpyDeviceToDevice, s->own_stream);
+    const hipError_t ef = hipFreeAsync(sorted, s->own_stream);
+    if (e == hipSuccess) e = ef;
+    if (e == hipSuccess) e = hipStreamSynchronize(s->own_stream);
+    if (e != hipSuccess) return cleanup(hip_fail(e, "device BVH build"));
+    hs.num_nodes = r.num_nodes;
+    hs.depth = r.depth;
+    hs.stack_need = r.stack_need;
+    gpu_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
+  }
 
   s->dev.nodes = reinterpret_cast<const float4*>(base + parts[0].off);
   s->dev.refs = reinterpret_cast<const int32_t*>(base + parts[1].off);
@@ -631,6 +670,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
       ident_q = ident_q && hs.refs[r] == (static_cast<int32_t>(r) | kQuadRefBit);
     }
     s->dev.ref_mode = ident_s ? 1 : (ident_q ? 2 : 0);
+    if (hs.gpu_bvh) s->dev.ref_mode = 0;  // the device build permuted the refs
   }
   s->dev.tex_full = 0;
   for (int32_t t = 0; t < desc->num_textures; ++t)
@@ -646,7 +686,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->info.stack_depth = hs.stack_need;
   s->stack_need = hs.stack_need;
   s->info.device_bytes = static_cast<int64_t>(total);
-  s->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  s->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() + gpu_build_ms;
   s->info.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
   *out = s;
   return RTG_OK;

@@ -39,8 +39,10 @@ struct HostScene {
   int64_t num_nodes = 0;
   int32_t depth = 0;
   int32_t stack_need = 0;  // traversal stack entries needed (<= depth for BVH2)
-  int32_t node_width = 2;  // 2: child-pair 64-B nodes, 4: 4-wide 128-B nodes
+  int32_t node_width = 2;  // 2: child-pair 64-B nodes, 4: 4-wide 112-B nodes
   int64_t num_prims = 0;
+  bool gpu_bvh = false;       // RTG_BVH_GPU: nodes are built on the device after the upload
+  int64_t node_capacity = 0;  // gpu_bvh: 4-wide nodes to reserve
 };
 
 // Double-precision BVH produced by the builders (child-pair form, pre-order DFS).
@@ -124,6 +126,14 @@ struct DevScene {
   int32_t tex_full;  // 1 when some texture is an image or noise texture (kernel variant selector)
   int32_t num_perlins;  // perlin tables (256 gradients + 3 x 256 permutations each)
 };
+
+struct GpuBvhResult {  // rtg_gpubvh.hip
+  int64_t num_nodes;
+  int32_t depth;
+  int32_t stack_need;
+};
+hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int32_t* refs_in, int64_t n,
+                          float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res, hipStream_t st);
 
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
 

@@ -25,7 +25,7 @@ RTG_OK = 0
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
 RTG_MAT_LAMBERTIAN, RTG_MAT_METAL, RTG_MAT_DIELECTRIC, RTG_MAT_DIFFUSE_LIGHT = 1, 2, 3, 4
 RTG_TEX_SOLID, RTG_TEX_CHECKER, RTG_TEX_IMAGE, RTG_TEX_NOISE = 1, 2, 3, 4
-RTG_BVH_MEDIAN, RTG_BVH_SAH = 0, 1
+RTG_BVH_MEDIAN, RTG_BVH_SAH, RTG_BVH_GPU = 0, 1, 3
 RTG_RENDER_OUT_DEVICE, RTG_RENDER_ASYNC, RTG_RENDER_COUNT = 0x1, 0x2, 0x4
 
 

@@ -274,6 +274,30 @@ def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypat
     ds.close()
 
 
+@pytest.mark.parametrize("name,W", [("bouncing_spheres", 96), ("cornell_box", 64), ("simple_light", 64),
+                                    ("quads", 48)])
+def test_device_bvh_build_matches_oracle(gpu_lib, scenes, oracle, name, W):
+    """RTG_BVH_GPU (Morton LBVH built on the device): a different tree, the
+    same image as the oracle (closest hits are order-free up to exact ties, H9)."""
+    g, o, st, segs = compare(gpu_lib, scenes, oracle, name, bvh=rtgpu.RTG_BVH_GPU, image_width=W,
+                             samples_per_pixel=4, max_depth=20)
+    exact = 0.0 if name == "simple_light" else 0.999
+    assert_parity(g, o, st, segs, exact_frac=exact)
+
+
+def test_device_bvh_build_million_spheres(gpu_lib, scenes, oracle):
+    s = scenes.build("bouncing_spheres", grid=500, rand_seed=1, bvh_mode=rtgpu.RTG_BVH_GPU)
+    ds = gpu_lib.scene_create(s.desc)
+    info = ds.info()
+    assert info.num_nodes > 1_000_001 // 8 and info.build_ms < 2000, (info.num_nodes, info.build_ms)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 64, 2, 50
+    g, st = ds.render_host(c)
+    ds.close()
+    o, segs = oracle.render_f32(s.desc, c)
+    assert_parity(g, o, st, segs)
+
+
 def test_million_sphere_scene(gpu_lib, scenes, oracle):
     """BASELINE config 5 scene (grid 500 -> 1,000,001 objects, deep BVH) at a small image."""
     g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", grid=500, image_width=64,

@@ -46,7 +46,7 @@ def main():
     if not libs:
         libs["lib"] = rtgpu.Library()
     first = next(iter(libs))
-    bvh = {"sah": rtgpu.RTG_BVH_SAH, "median": rtgpu.RTG_BVH_MEDIAN, "sah2": 2}[a.bvh]
+    bvh = {"sah": rtgpu.RTG_BVH_SAH, "median": rtgpu.RTG_BVH_MEDIAN, "sah2": 2, "gpu": 3}[a.bvh]
     s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
                                    spp=a.spp, max_depth=a.depth, bvh_mode=bvh)
     cam = s.camera

@@ -4,9 +4,12 @@
 // C-ABI of librtgpu (include/rtgpu.h) and runs the per-pixel sample loop on the MI355X, then
 // writes the same P3 PPM. There is no CPU fallback: any device or scene error throws.
 #pragma once
+#include <algorithm>
 #include <cstdio>
+#include <exception>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "core/material.hpp"
@@ -27,11 +30,15 @@ class device_scene {
  public:
   device_scene(const hittable& world, int device = 0, int bvh_mode = RTG_BVH_SAH) {
     scene_builder sb;
+    flatten(world, sb);
+    const rtg_scene_desc d = sb.desc(bvh_mode);
+    check(rtg_scene_create(&d, device, &scene_), "rtg_scene_create");
+  }
+  device_scene(const rtg_scene_desc& d, int device) { check(rtg_scene_create(&d, device, &scene_), "rtg_scene_create"); }
+  static void flatten(const hittable& world, scene_builder& sb) {
     if (!world.rtg_flatten(sb, vec3(0, 0, 0)))
       throw std::runtime_error("rtgpu: world cannot be flattened for the device: " +
                                (sb.error.empty() ? std::string("unsupported hittable") : sb.error));
-    const rtg_scene_desc d = sb.desc(bvh_mode);
-    check(rtg_scene_create(&d, device, &scene_), "rtg_scene_create");
   }
   ~device_scene() { rtg_scene_destroy(scene_); }
   device_scene(const device_scene&) = delete;
@@ -63,6 +70,7 @@ class camera {
   // ---- extensions (not in the reference) ----
   uint64_t seed = 0x5EED;          // counter-RNG run seed
   int device = 0;                  // HIP device to render on
+  std::vector<int> devices;        // > 1 entries: row-interleaved shards on these devices (threads)
   int bvh_mode = RTG_BVH_SAH;      // device BVH builder
   rtg_render_stats last_stats{};   // segments, samples, kernel time of the last render
 
@@ -70,15 +78,88 @@ class camera {
     const std::vector<float> rgb = render_linear(world);
     const int H = image_height();
     output_stream << "P3\n" << image_width << ' ' << H << "\n255\n";
-    for (size_t k = 0; k + 2 < rgb.size(); k += 3) write_color(output_stream, color(rgb[k], rgb[k + 1], rgb[k + 2]));
+    write_ppm_body(output_stream, rgb);
     std::printf("\rDone.                       \n");
     std::fflush(stdout);
   }
 
   // The linear, pre-gamma per-pixel mean (what the reference hands to write_color), H*W*3.
   std::vector<float> render_linear(const hittable& world) {
+    if (devices.size() > 1) return render_linear_multi(world);
     rtgpu::device_scene scene(world, device, bvh_mode);
     return render_linear(scene);
+  }
+
+  // write_color (color.hpp:26-58) for every pixel, the text formatted on all host cores and
+  // written in order: the same bytes as the reference's per-pixel stream writes.
+  static void write_ppm_body(std::ostream& out, const std::vector<float>& rgb) {
+    const size_t n = rgb.size() / 3;
+    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const size_t parts = std::max<size_t>(1, std::min<size_t>(hw, n / 4096));
+    std::vector<std::string> text(parts);
+    auto work = [&](size_t t) {
+      std::string& s = text[t];
+      const size_t b = n * t / parts, e = n * (t + 1) / parts;
+      s.reserve((e - b) * 12);
+      char buf[16];
+      for (size_t k = b; k < e; ++k) {
+        static const interval intensity(0.000f, 0.999f);
+        for (int c = 0; c < 3; ++c) {
+          const int v = int(256 * intensity.clamp(linear_to_gamma(rgb[3 * k + c])));
+          const int len = std::snprintf(buf, sizeof(buf), c < 2 ? "%d " : "%d\n", v);
+          s.append(buf, static_cast<size_t>(len));
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < parts; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    for (const std::string& s : text) out.write(s.data(), static_cast<std::streamsize>(s.size()));
+  }
+
+  // One host thread per entry of `devices`: device r renders rows r, r+N, ... (the RNG is keyed
+  // by the global pixel, so the frame is identical to a single-device render).
+  std::vector<float> render_linear_multi(const hittable& world) {
+    rtgpu::scene_builder sb;
+    rtgpu::device_scene::flatten(world, sb);
+    const rtg_scene_desc d = sb.desc(bvh_mode);
+    const rtg_camera_desc cd = desc();
+    const int N = static_cast<int>(devices.size()), H = image_height(), W = image_width;
+    std::vector<std::vector<float>> shard(N);
+    std::vector<rtg_render_stats> st(N);
+    std::vector<std::exception_ptr> errs(N);
+    std::vector<std::thread> pool;
+    for (int r = 0; r < N; ++r)
+      pool.emplace_back([&, r] {
+        try {
+          rtgpu::device_scene scene(d, devices[r]);
+          const int rows = r < H ? (H - 1 - r) / N + 1 : 0;
+          shard[r].assign(static_cast<size_t>(rows) * W * 3, 0.0f);
+          if (rows == 0) return;
+          rtg_render_desc job{};
+          job.seed = seed;
+          job.row_begin = r;
+          job.row_stride = N;
+          rtgpu::check(rtg_render(scene.handle(), &cd, &job, shard[r].data(), &st[r]), "rtg_render");
+        } catch (...) {
+          errs[r] = std::current_exception();
+        }
+      });
+    for (auto& th : pool) th.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+    std::vector<float> rgb(static_cast<size_t>(H) * W * 3);
+    last_stats = rtg_render_stats{};
+    for (int r = 0; r < N; ++r) {
+      for (size_t k = 0; k * W * 3 < shard[r].size(); ++k)
+        std::copy(shard[r].begin() + k * W * 3, shard[r].begin() + (k + 1) * W * 3,
+                  rgb.begin() + (static_cast<size_t>(r) + k * N) * W * 3);
+      last_stats.segments += st[r].segments;
+      last_stats.samples += st[r].samples;
+      last_stats.kernel_ms = std::max(last_stats.kernel_ms, st[r].kernel_ms);
+    }
+    return rgb;
   }
   std::vector<float> render_linear(const rtgpu::device_scene& scene) {
     const rtg_camera_desc cd = desc();

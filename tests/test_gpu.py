@@ -362,3 +362,8 @@ def test_raytracer_cli_writes_ppm(tmp_path):
     assert tokens[:4] == ["P3", "64", "64", "255"]
     vals = np.array(tokens[4:], dtype=int)
     assert vals.size == 64 * 64 * 3 and vals.min() >= 0 and vals.max() <= 255 and vals.max() > 0
+    # rows split over several devices (here the same GPU twice, one host thread each): same bytes
+    out2 = tmp_path / "cornell2.ppm"
+    subprocess.run([exe, str(out2), "cornell_box", "64", "8", "20", "0,0,0"], check=True, timeout=120,
+                   capture_output=True)
+    assert out2.read_bytes() == out.read_bytes()

@@ -248,3 +248,32 @@ def test_reference_main_compiles_against_mirror(tmp_path):
                         "-o", str(tmp_path / "main.o")], stdin=src, check=True, cwd=tmp_path)
     subprocess.run(["g++", str(tmp_path / "main.o"), f"-L{REPO}/raytracing-practice_amd/lib",
                     "-lrtgpu", "-o", str(tmp_path / "raytracer")], check=True)
+
+
+def test_parallel_ppm_body_matches_write_color(tmp_path):
+    """camera::write_ppm_body (threads format the P3 text) writes exactly the bytes of the
+    reference's per-pixel write_color stream (color.hpp:26-58)."""
+    src = tmp_path / "ppm.cpp"
+    src.write_text(r'''
+#include <cstdio>
+#include <random>
+#include <sstream>
+#include "core/camera.hpp"
+int main() {
+  std::mt19937 g(7);
+  std::uniform_real_distribution<float> u(-0.1f, 1.4f);
+  std::vector<float> rgb(3 * 50000);
+  for (float& x : rgb) x = u(g);
+  rgb[0] = 0.0f; rgb[1] = 0.998001f; rgb[2] = 1e-9f;
+  std::ostringstream a, b;
+  camera::write_ppm_body(a, rgb);
+  for (size_t k = 0; k < rgb.size(); k += 3) write_color(b, color(rgb[k], rgb[k + 1], rgb[k + 2]));
+  std::printf("%d %zu\n", a.str() == b.str() ? 1 : 0, a.str().size());
+  return a.str() == b.str() ? 0 : 1;
+}
+''')
+    inc = [f"-I{REPO}/raytracing-practice_amd/include", f"-I{REPO}/include"]
+    subprocess.run(["g++", "-std=c++17", "-O1", *inc, str(src), "-pthread", "-o", str(tmp_path / "ppm")],
+                   check=True)
+    r = subprocess.run([str(tmp_path / "ppm")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout

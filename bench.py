@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--bvh", choices=["sah", "median", "gpu"], default="sah")
     ap.add_argument("--seed", type=int, default=0x5EED)
+    ap.add_argument("--gather", choices=["f32", "rgb8"], default="f32",
+                    help="gather the linear fp32 frame (default) or the write_color bytes (4x fewer)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=None,
                     help="spp of the bounded CPU sample (default 8; 2 for the 4K config 5)")
@@ -142,13 +144,16 @@ def main():
     info = ds.info()
     b, stride, n = rtgpu.shard_rows(H, rank, world)
     shard = torch.zeros((rtgpu.padded_rows(H, world), W, 3), dtype=torch.float32, device="cuda")
+    shard8 = torch.zeros(shard.shape, dtype=torch.uint8, device="cuda") if args.gather == "rgb8" else None
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(i):
         st = ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + i, row_begin=b,
                               row_stride=stride, row_count=n)
+        if shard8 is not None:  # write_color on the device (rtg_resolve_rgb8), gather the bytes
+            ds.resolve_rgb8(shard.data_ptr(), shard8.data_ptr(), shard.shape[0] * W, stream)
         if world > 1:
-            rtgpu.gather_frame(shard, H)
+            rtgpu.gather_frame(shard8 if shard8 is not None else shard, H)
         return st
 
     for i in range(args.warmup):
@@ -202,7 +207,7 @@ def main():
             "config": {"workload": workload, "baseline_config": args.config, "scene": args.scene,
                        "grid": args.grid, "width": W,
                        "height": H, "spp": args.spp, "depth": args.depth, "bvh": args.bvh,
-                       "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather to rank 0"},
+                       "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather ({args.gather}) to rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic(workload),

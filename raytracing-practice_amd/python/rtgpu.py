@@ -401,6 +401,18 @@ def camera(**kw) -> rtg_camera_desc:
     return c
 
 
+def write_color_bytes(rgb):
+    """write_color (color.hpp:26-58) on a float array (..., 3): sqrt gamma (in double, as the
+    reference's linear_to_gamma), clamp to [0, 0.999], int(256 * x) -> uint8. Host twin of
+    rtg_resolve_rgb8 for CPU-side shards."""
+    import numpy as np
+
+    x = np.asarray(rgb, dtype=np.float64)
+    x = np.where(x > 0.0, np.sqrt(np.maximum(x, 0.0)), 0.0)
+    x = np.clip(x, 0.0, np.float64(np.float32(0.999)))
+    return (256.0 * x).astype(np.int32).astype(np.uint8)
+
+
 def gather_frame(shard, height: int, dst: int = 0):
     """Collect every rank's interleaved shard on `dst` and de-interleave.
 

@@ -36,10 +36,14 @@ def _worker(rank, world, port, result_path):
             img, _ = Oracle().render_f32(s.desc, cam, row_begin=b, row_stride=stride, row_count=n)
             shard[:n] = torch.from_numpy(img)
         frame = rtgpu.gather_frame(shard, H)
+        # the RGB8 variant: write_color bytes gathered, 4x fewer bytes
+        bytes8 = torch.from_numpy(np.stack([rtgpu.write_color_bytes(r) for r in shard.numpy()]))
+        frame8 = rtgpu.gather_frame(bytes8, H)
         if rank == 0:
             np.save(result_path, frame.numpy())
+            np.save(result_path + ".rgb8.npy", frame8.numpy())
         else:
-            assert frame is None
+            assert frame is None and frame8 is None
     finally:
         dist.destroy_process_group()
 
@@ -57,6 +61,8 @@ def test_gloo_sharded_render_equals_single(tmp_path, world, scenes, oracle, lib)
     full, _ = oracle.render_f32(s.desc, cam)
     assert frame.shape == full.shape
     assert np.array_equal(frame, full)
+    frame8 = np.load(out + ".rgb8.npy")
+    assert frame8.dtype == np.uint8 and np.array_equal(frame8, rtgpu.write_color_bytes(full))
 
 
 def test_shard_rows_cover_the_image():

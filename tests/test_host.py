@@ -277,3 +277,14 @@ int main() {
                    check=True)
     r = subprocess.run([str(tmp_path / "ppm")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout
+
+
+def test_write_color_bytes_matches_oracle(oracle):
+    """rtgpu.write_color_bytes (the host twin of rtg_resolve_rgb8, used for RGB8 gathers) equals
+    the oracle's write_color, itself pinned to the reference (test_oracle_golden)."""
+    rng = np.random.default_rng(3)
+    vals = np.concatenate([rng.uniform(-0.2, 1.3, 3000), [0.0, 0.998001, 0.99800104, 1e-12, 1.0]])
+    vals = vals.astype(np.float32)
+    got = rtgpu.write_color_bytes(vals.reshape(-1, 1).repeat(3, axis=1))[:, 0]
+    want = [oracle.write_color([float(v)] * 3)[0] for v in vals]
+    assert np.array_equal(got.astype(int), np.array(want))

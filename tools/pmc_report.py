@@ -29,6 +29,18 @@ def load(path, kernel_filter):
     return per, meta
 
 
+def is_count_variant(name):
+    """True for the RTG_RENDER_COUNT instantiation: COUNT is template argument 3 of
+    render_kernel / render_kernel_lds <STACK, SPILL, COUNT, ...> and argument 2 of the A/B kernels
+    render_kernel_v0 / render_kernel_segment <STACK, COUNT>."""
+    m = re.search(r"(render_kernel\w*)<([^>]*)>", name)
+    if not m:
+        return False
+    args = [x.strip() for x in m.group(2).split(",")]
+    idx = 1 if m.group(1) in ("render_kernel_v0", "render_kernel_segment") else 2
+    return len(args) > idx and args[idx] == "true"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir", nargs="?", default="gpurun_out/prof")
@@ -46,7 +58,7 @@ def main():
         per, meta = load(p, a.kernel)
         for d, vals in per.items():
             name = meta[d][0]
-            if a.timed_only and re.search(r"<\d+, true", name):
+            if a.timed_only and is_count_variant(name):
                 continue  # RTG_RENDER_COUNT variant
             for k, v in vals.items():
                 counters.setdefault(k, []).append(v)

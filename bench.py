@@ -186,7 +186,8 @@ def main():
                   + BYTES_PER_HIT * cst.hits)
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     achieved = algo_bytes / avg_kernel_s / 1e9
-    workload = f"{args.scene}(grid={args.grid}) {W}x{H} {args.spp}spp depth{args.depth} bvh={args.bvh}"
+    workload = (f"{args.scene}(grid={args.grid}) {W}x{H} {args.spp}spp depth{args.depth} bvh={args.bvh} "
+                f"chunk={rtgpu.chunk_samples(args.spp)}")
 
     if rank == 0:
         samples = W * H * args.spp * args.steps

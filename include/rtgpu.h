@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 3
+#define RTG_ABI_VERSION 4
 
 typedef int32_t rtg_status;
 #define RTG_OK 0
@@ -165,10 +165,12 @@ typedef struct rtg_camera_params {
 /* rtg-f32 per-pixel accumulation (DESIGN.md §4 "sample chunks"): a pixel's samples are summed in
  * chunks of K = rtg_chunk_samples(spp) consecutive samples, each chunk in sample order starting from
  * zero, and the chunk sums are then added in chunk order; the pixel is pixel_samples_scale * that.
- * spp <= 64 gives one chunk, i.e. the reference's single running sum (camera.hpp:55-62). Chunks are
- * the device's unit of work, so one expensive pixel never holds a wavefront for all its samples. */
+ * spp <= 16 gives one chunk, i.e. the reference's single running sum (camera.hpp:55-62). Chunks are
+ * the device's unit of work, so one expensive pixel never holds a wavefront for all its samples, and
+ * the last units of a frame (or of a 1/8 shard of one) end close together (ABI 4: 16, was 64). */
+#define RTG_CHUNK_MAX 16
 static inline int rtg_chunk_samples(int spp) {
-  int n = (spp + 63) / 64;
+  int n = (spp + RTG_CHUNK_MAX - 1) / RTG_CHUNK_MAX;
   if (n < 1) n = 1;
   return spp > 0 ? (spp + n - 1) / n : 1;
 }

@@ -794,8 +794,15 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const int leaf_batch = (job->flags >> 24) & 0x7f;
   dj.leaf_batch = leaf_batch == 0 ? kDefaultLeafBatch : (leaf_batch > 64 ? 64 : leaf_batch);
   dj.out = dout;
-  dj.tiles_x = (W + 7) / 8;
-  dj.num_tiles = dj.tiles_x * ((rows + 7) / 8);
+  // tile shape: 8x8 pixels of a contiguous image; wider and flatter tiles for row-interleaved shards,
+  // whose consecutive shard rows lie row_stride image rows apart (keeps a wave's rays coherent)
+  dj.tile_lw = job->row_stride <= 1 ? 3 : 4;
+  if (const char* e = std::getenv("RTG_TILE_LW")) dj.tile_lw = std::min(6, std::max(0, std::atoi(e)));
+  {
+    const int tw = 1 << dj.tile_lw, th = 64 / tw;
+    dj.tiles_x = (W + tw - 1) / tw;
+    dj.num_tiles = dj.tiles_x * ((rows + th - 1) / th);
+  }
   dj.chunk_samples = rtg_chunk_samples(cam->samples_per_pixel);
   // RTG_CHUNK_SAMPLES overrides K for schedule experiments (the frame then differs from the spec)
   if (const char* e = std::getenv("RTG_CHUNK_SAMPLES")) dj.chunk_samples = std::max(1, std::atoi(e));

@@ -148,8 +148,9 @@ struct DevJob {
   // [6] persistent kernels' tile counter, [8..23] schedule diagnostics
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
-  int32_t tiles_x;    // 8x8 pixel tiles per shard row of tiles
-  int32_t num_tiles;  // 8x8 pixel tiles in the shard; work is handed out in 4x4 quarters of them
+  int32_t tiles_x;    // 64-pixel tiles per shard row of tiles
+  int32_t num_tiles;  // 64-pixel tiles in the shard (one wave's batch: a tile and a sample chunk)
+  int32_t tile_lw;    // log2 tile width: 3 = 8x8 shard pixels, 4 = 16x4, 5 = 32x2 (row-strided shards)
   int32_t chunks;         // sample chunks rendered by this launch (work units = pixel x chunk)
   int32_t chunk_begin;    // first of them (progressive rendering; 0 for a one-shot frame)
   int32_t pad4_;

@@ -877,6 +877,10 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   uint32_t px = 0;
   int sample = 0, s_end = 0, chunk = 0;
   bool has = false;
+  // fresh: the lane starts sample `sample` of its unit at the top of the next loop trip (the one
+  // start path for the next sample of a unit and the first sample of a new unit); cont: its path
+  // continues with a new segment (ps.o / ps.d scattered)
+  bool fresh = false, cont = false;
   // wave-uniform: the current batch's tile origin and chunk, and its next unassigned unit
   int bx = 0, by = 0, bc = 0, k_next = 64;
   bool exhausted = false;
@@ -899,8 +903,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         const int tile = b / J.chunks;
         bc = J.chunk_begin + (b - tile * J.chunks);
         const int ty = tile / J.tiles_x;
-        bx = (tile - ty * J.tiles_x) * 8;
-        by = ty * 8;
+        bx = (tile - ty * J.tiles_x) << J.tile_lw;
+        by = ty << (6 - J.tile_lw);
         k_next = 0;
       }
       const int take = min(__popcll(want), 64 - k_next);
@@ -908,8 +912,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           static_cast<uint32_t>(want >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(want), 0u)));
       if (!has && rank < take) {
         const int k = k_next + rank;
-        const int i = bx + (k & 7);
-        const int lr = by + (k >> 3);
+        const int i = bx + (k & ((1 << J.tile_lw) - 1));
+        const int lr = by + (k >> J.tile_lw);
         if (i < C.width && lr < J.row_count) {
           px = static_cast<uint32_t>(i) | (static_cast<uint32_t>(lr) << 16);
           if (no_work) {
@@ -919,18 +923,21 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
             }
           } else {
             has = true;
+            fresh = true;
             chunk = bc;
             sample = bc * J.chunk_samples;
             s_end = min(sample + J.chunk_samples, C.spp);
             acc = v3(0.0f, 0.0f, 0.0f);
-            start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
-            trav_begin(tr, S, ps.o, ps.d);
           }
         }
       }
       k_next += take;
       want = __ballot(!has);
     }
+    if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
+    if (fresh || cont) trav_begin(tr, S, ps.o, ps.d);
+    fresh = false;
+    cont = false;
     const int alive = __popcll(__ballot(has));
     if (alive == 0) break;
     const int need = (alive * J.shade_batch + 63) >> 6;
@@ -993,11 +1000,12 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         t_end = __builtin_amdgcn_s_memtime();
         w.diag[11] += t_end - t_shade0;
       }
+      cont = alive_path;
       if (!alive_path) {
         acc = add(acc, ps.L);
         ++sample;
         if (sample < s_end) {
-          start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
+          fresh = true;
         } else {
           const int64_t pix = static_cast<int64_t>(px_lr(px)) * C.width + px_i(px);
           if (J.partial == nullptr) {  // one chunk per pixel: the pixel mean directly
@@ -1015,13 +1023,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           ++w.pixels;
         }
       }
-      uint64_t t_tb = 0;
-      if (COUNT) {
-        t_tb = __builtin_amdgcn_s_memtime();
-        w.diag[12] += t_tb - t_end;
-      }
-      if (has) trav_begin(tr, S, ps.o, ps.d);
-      if (COUNT) w.diag[13] += __builtin_amdgcn_s_memtime() - t_tb;
+      if (COUNT) w.diag[12] += __builtin_amdgcn_s_memtime() - t_end;
     }
     if (COUNT) w.diag[6] += __builtin_amdgcn_s_memtime() - t_shade0;
   }

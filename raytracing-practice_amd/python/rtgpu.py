@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 
-RTG_ABI_VERSION = 3
+RTG_ABI_VERSION = 4
 RTG_OK = 0
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
 RTG_MAT_LAMBERTIAN, RTG_MAT_METAL, RTG_MAT_DIELECTRIC, RTG_MAT_DIFFUSE_LIGHT = 1, 2, 3, 4
@@ -138,7 +138,7 @@ def _P(t):
 
 def chunk_samples(spp: int) -> int:
     """rtgpu.h rtg_chunk_samples: samples per accumulation chunk of the rtg-f32 spec."""
-    n = max(1, (spp + 63) // 64)
+    n = max(1, (spp + 15) // 16)  # RTG_CHUNK_MAX
     return (spp + n - 1) // n if spp > 0 else 1
 
 

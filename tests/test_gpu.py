@@ -138,12 +138,20 @@ def test_shards_and_determinism(gpu_lib, scenes):
         assert np.array_equal(rtgpu.deinterleave(shards, H), full)
     other, _ = ds.render_host(c, seed=100)
     assert not np.array_equal(other, full)
+    # several sample chunks per pixel and the strided shards' 16x4 tiles: still bit-identical
+    c.image_width, c.samples_per_pixel = 96, 40
+    full, _ = ds.render_host(c, seed=5)
+    H = full.shape[0]
+    for world in (2, 8):
+        shards = [ds.render_host(c, seed=5, row_begin=b, row_stride=stride, row_count=n)[0]
+                  for b, stride, n in (rtgpu.shard_rows(H, r, world) for r in range(world))]
+        assert np.array_equal(rtgpu.deinterleave(shards, H), full)
     ds.close()
 
 
-@pytest.mark.parametrize("spp", [65, 130, 200])
+@pytest.mark.parametrize("spp", [17, 65, 200])
 def test_sample_chunks_match_oracle(gpu_lib, scenes, oracle, spp):
-    """Above 64 spp a pixel's samples are accumulated in chunks (rtgpu.h rtg_chunk_samples) that the
+    """Above 16 spp a pixel's samples are accumulated in chunks (rtgpu.h rtg_chunk_samples) that the
     device renders as separate work units and combines in chunk order: bit-identical to cpu_ref32."""
     g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", image_width=48,
                              samples_per_pixel=spp, max_depth=20)
@@ -162,10 +170,10 @@ def test_progressive_chunks_and_checkpoint(gpu_lib, scenes):
 
     s = scenes.build("bouncing_spheres", rand_seed=1)
     c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
-    c.image_width, c.samples_per_pixel, c.max_depth = 80, 200, 20
-    n = rtgpu.num_chunks(200)
-    K = rtgpu.chunk_samples(200)
-    assert (n, K) == (4, 50)
+    c.image_width, c.samples_per_pixel, c.max_depth = 80, 60, 20
+    n = rtgpu.num_chunks(60)
+    K = rtgpu.chunk_samples(60)
+    assert (n, K) == (4, 15)
     ds = gpu_lib.scene_create(s.desc)
     full, _ = ds.render_host(c, seed=7)
     H = full.shape[0]

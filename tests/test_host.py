@@ -29,12 +29,14 @@ def test_cabi_exports_every_declared_symbol(lib):
 
 
 def test_chunk_rule():
-    """rtg_chunk_samples (rtgpu.h): one chunk up to 64 spp, chunks of <= 64 samples above."""
+    """rtg_chunk_samples (rtgpu.h): one chunk up to 16 spp, chunks of <= 16 samples above."""
     def k(spp):
-        n = max(1, (spp + 63) // 64)
+        n = max(1, (spp + 15) // 16)
         return (spp + n - 1) // n if spp > 0 else 1
-    assert [k(s) for s in (1, 10, 64, 65, 500, 1000, 2000)] == [1, 10, 64, 33, 63, 63, 63]
-    assert rtgpu.chunk_samples(500) == 63 and rtgpu.chunk_samples(64) == 64
+    assert [k(s) for s in (1, 10, 16, 17, 64, 500, 1000, 2000)] == [1, 10, 16, 9, 16, 16, 16, 16]
+    assert [rtgpu.chunk_samples(s) for s in (1, 10, 16, 17, 64, 500, 1000, 2000)] == \
+        [k(s) for s in (1, 10, 16, 17, 64, 500, 1000, 2000)]
+    assert rtgpu.num_chunks(500) == 32 and rtgpu.num_chunks(16) == 1
 
 
 def test_scenes_lib_exports(scenes):

@@ -32,6 +32,11 @@ constexpr int kMaxStackNeed = 4096;     // traversal stack entries per lane (LDS
 constexpr int kPlainWgsPerCu = 5;        // schedule 4 grid: resident workgroups per CU (waves pull work)
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
 constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
+// Scenes with a handful of BVH nodes (Cornell's 18 quads, earth + perlin's 2 spheres) reach their
+// leaves after one or two node steps, so waiting for more lanes there costs little and fills the
+// (expensive: quads, textures) leaf trips: Cornell -15 %, earth_perlin -1.5 % (profiles/r01_leafbatch)
+constexpr int kSmallBvhNodes = 16;
+constexpr int kSmallBvhLeafBatch = 48;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
 }
@@ -792,7 +797,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const int batch = (job->flags >> 16) & 0xff;
   dj.shade_batch = batch == 0 ? kDefaultShadeBatch : (batch > 64 ? 64 : batch);
   const int leaf_batch = (job->flags >> 24) & 0x7f;
-  dj.leaf_batch = leaf_batch == 0 ? kDefaultLeafBatch : (leaf_batch > 64 ? 64 : leaf_batch);
+  const int default_leaf_batch = s->dev.num_nodes <= kSmallBvhNodes ? kSmallBvhLeafBatch : kDefaultLeafBatch;
+  dj.leaf_batch = leaf_batch == 0 ? default_leaf_batch : (leaf_batch > 64 ? 64 : leaf_batch);
   dj.out = dout;
   // tile shape: 8x8 pixels of a contiguous image; wider and flatter tiles for row-interleaved shards,
   // whose consecutive shard rows lie row_stride image rows apart (keeps a wave's rays coherent)

@@ -661,6 +661,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.perlin_vec = reinterpret_cast<const float4*>(base + parts[8].off);
   s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
   s->dev.num_nodes = hs.num_nodes;
+  s->dev.root_code = 0;
+  s->dev.node_limit = static_cast<int32_t>(std::min<int64_t>(hs.num_nodes * 112, INT32_MAX));
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
   s->dev.num_quads = static_cast<int64_t>(hs.quads.size() / 20);

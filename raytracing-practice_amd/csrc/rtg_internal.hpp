@@ -125,6 +125,11 @@ struct DevScene {
   int32_t ref_mode;
   int32_t tex_full;  // 1 when some texture is an image or noise texture (kernel variant selector)
   int32_t num_perlins;  // perlin tables (256 gradients + 3 x 256 permutations each)
+  // 4-wide trees: inner-node codes are byte offsets from `nodes`, the root's is root_code (0 in
+  // HBM; the persistent kernel rebases its LDS copy so codes are absolute LDS addresses) and every
+  // valid one is below node_limit (root_code + num_nodes * 112)
+  int32_t root_code;
+  int32_t node_limit;
 };
 
 struct GpuBvhResult {  // rtg_gpubvh.hip

@@ -183,7 +183,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.oz = -o.z * t.iz;
   t.tbest = __builtin_inff();
   t.best = -1;
-  t.todo = 0;
+  t.todo = S.root_code;
   t.sp = 0;
   t.active = S.num_nodes > 0;
 }
@@ -280,6 +280,14 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, const Stk&
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float nf4 __attribute__((ext_vector_type(4)));
+// LDS loads from 32-bit LDS byte addresses (no generic-pointer base arithmetic)
+__device__ __forceinline__ nf4 lds_ld4(uint32_t a) {
+  return *reinterpret_cast<__attribute__((address_space(3))) const nf4*>(static_cast<uintptr_t>(a));
+}
+__device__ __forceinline__ int32_t lds_ld1(uint32_t a) {
+  return *reinterpret_cast<__attribute__((address_space(3))) const int32_t*>(static_cast<uintptr_t>(a));
+}
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Entry distance of one child (tn) or a miss: the slab test with the near/far planes already
@@ -320,19 +328,20 @@ template <class Stk, bool COUNT, bool PAIRS>
 __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
   // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
-  if (t.todo >= S.num_nodes * 112) {
+  if (t.todo >= S.node_limit) {
     corrupt = true;
     t.active = false;
     return;
   }
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
   const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
-  const float4 nx = *reinterpret_cast<const float4*>(nb + sx);
-  const float4 ny = *reinterpret_cast<const float4*>(nb + 16 + sy);
-  const float4 nz = *reinterpret_cast<const float4*>(nb + 32 + sz);
-  const float4 fx = *reinterpret_cast<const float4*>(nb + 48 - sx);
-  const float4 fy = *reinterpret_cast<const float4*>(nb + 64 - sy);
-  const float4 fz = *reinterpret_cast<const float4*>(nb + 80 - sz);
+  const uint32_t na = static_cast<uint32_t>(t.todo);  // LDS scenes: the node's LDS address
+  auto row = [&](int32_t off) -> nf4 {
+    if constexpr (PAIRS) return *reinterpret_cast<const nf4*>(nb + off);
+    else return lds_ld4(na + static_cast<uint32_t>(off));
+  };
+  const nf4 nx = row(sx), ny = row(16 + sy), nz = row(32 + sz);
+  const nf4 fx = row(48 - sx), fy = row(64 - sy), fz = row(80 - sz);
   if (COUNT) cnt.box += 4;
   const f2 ix = {t.ix, t.ix}, iy = {t.iy, t.iy}, iz = {t.iz, t.iz};
   const f2 ox = {t.ox, t.ox}, oy = {t.oy, t.oy}, oz = {t.oz, t.oz};
@@ -380,10 +389,13 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
       trav_pop(t, stk);
       return;
     }
-    const char* codes = nb + 96;
-    auto code_of = [&](uint32_t k) { return *reinterpret_cast<const int32_t*>(codes + (k & 12u)); };
+    // node addresses are 16-byte aligned (112-byte nodes from an aligned base), so the code of
+    // slot (k & 12) / 4 is at (node | (k & 12)) + 96: one v_and_or per code
+    auto code_of = [&](uint32_t k) { return lds_ld1((na | (k & 12u)) + 96u); };
+    // the host sizes every stack from the tree's structural bound (sum of siblings along a path,
+    // Bvh4::max_pushes), so pushes cannot overflow; the check runs in the COUNT diagnostics only
     const int npush = (k1 != ~0u) + (k2 != ~0u) + (k3 != ~0u);
-    if (t.sp + npush > stk.capacity()) {
+    if (COUNT && t.sp + npush > stk.capacity()) {
       overflow = true;
     } else {
       if (k3 != ~0u) stk.store(t.sp++, code_of(k3));
@@ -1071,7 +1083,21 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   float4* l_textures = reinterpret_cast<float4*>(smem + J.lds_textures);
   for (int k = threadIdx.x; k < S.num_materials * 2; k += WAVES * 64) l_materials[k] = S.materials[k];
   for (int k = threadIdx.x; k < S.num_textures * 2; k += WAVES * 64) l_textures[k] = S.textures[k];
-  for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) l_nodes[k] = S.nodes[k];
+  // LDS byte address of the node array (inner-node codes of the LDS copy are rebased onto it)
+  const int32_t node_rebase = static_cast<int32_t>(static_cast<uint32_t>(
+      reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) unsigned char*)smem))) + J.lds_nodes;
+  for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) {
+    float4 v = S.nodes[k];
+    if (WIDE == 4 && k % 7 == 6) {  // code row: inner-node codes become absolute LDS addresses
+      int4 c = *reinterpret_cast<int4*>(&v);
+      c.x = c.x >= 0 ? c.x + node_rebase : c.x;
+      c.y = c.y >= 0 ? c.y + node_rebase : c.y;
+      c.z = c.z >= 0 ? c.z + node_rebase : c.z;
+      c.w = c.w >= 0 ? c.w + node_rebase : c.w;
+      v = *reinterpret_cast<float4*>(&c);
+    }
+    l_nodes[k] = v;
+  }
   for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64) l_spheres[k] = S.spheres[k];
   for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
   if (S.ref_mode == 0)
@@ -1085,6 +1111,10 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
+  if (WIDE == 4) {  // inner-node codes are absolute LDS byte addresses
+    L.root_code = node_rebase;
+    L.node_limit = node_rebase + static_cast<int32_t>(S.num_nodes) * 112;
+  }
   L.refs = l_refs;
   L.spheres = l_spheres;
   L.quads = l_quads;

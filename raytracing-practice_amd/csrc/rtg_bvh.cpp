@@ -9,6 +9,7 @@
 // traversal tests the two boxes the reference's left->hit / right->hit would test.
 //
 // RTG_BVH_SAH is this library's own binned-SAH builder (16 bins on centroids, leaves <= 4).
+#include <array>
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -311,13 +312,12 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
     }
     return sl;
   };
-  // recursive collapse; returns the new node index; tracks depth and stack pushes on the path
+  // recursive collapse into pre-allocated nodes; tracks depth and stack pushes on the path
   struct Rec {
     const Bvh& bin;
     Bvh4* out;
     decltype(slot_of)& slot;
-    int32_t go(int32_t b, int depth, int pushes) {
-      out->depth = std::max(out->depth, depth);
+    std::vector<Slot> gather(int32_t b) {
       std::vector<Slot> slots;
       const BuildNode& n = bin.nodes[b];
       for (int side = 0; side < 2; ++side)
@@ -342,13 +342,28 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
         slots.erase(slots.begin() + best);
         slots.insert(slots.begin() + best, kids.begin(), kids.end());
       }
-      const int32_t me = static_cast<int32_t>(out->nodes.size());
-      out->nodes.push_back(BuildNode4{});
+      return slots;
+    }
+    std::array<int32_t, 4> children(const std::vector<Slot>& slots, int depth, int pushes) {
+      out->depth = std::max(out->depth, depth);
       const int here = pushes + static_cast<int>(slots.size()) - 1;
       out->max_pushes = std::max(out->max_pushes, here);
-      int32_t codes[4] = {kEmptyChild, kEmptyChild, kEmptyChild, kEmptyChild};
+      std::array<int32_t, 4> codes = {kEmptyChild, kEmptyChild, kEmptyChild, kEmptyChild};
+      // the inner children of a node are allocated next to each other (then filled depth-first),
+      // so the siblings a ray visits after the nearest one share its cache lines
+      int32_t slot_ids[4] = {-1, -1, -1, -1};
       for (size_t i = 0; i < slots.size(); ++i)
-        codes[i] = slots[i].code >= 0 ? go(slots[i].code, depth + 1, here) : slots[i].code;
+        if (slots[i].code >= 0) {
+          slot_ids[i] = static_cast<int32_t>(out->nodes.size());
+          out->nodes.push_back(BuildNode4{});
+        }
+      for (size_t i = 0; i < slots.size(); ++i)
+        codes[i] = slots[i].code >= 0 ? fill(slot_ids[i], slots[i].code, depth + 1, here) : slots[i].code;
+      return codes;
+    }
+    int32_t fill(int32_t me, int32_t b, int depth, int pushes) {
+      std::vector<Slot> slots = gather(b);
+      std::array<int32_t, 4> codes = children(slots, depth, pushes);
       BuildNode4& o = out->nodes[me];
       for (int i = 0; i < 4; ++i) {
         o.child[i] = codes[i];
@@ -361,7 +376,8 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
       return me;
     }
   } rec{bin, out, slot_of};
-  rec.go(0, 1, 0);
+  out->nodes.push_back(BuildNode4{});  // the root is node 0
+  rec.fill(0, 0, 1, 0);
 }
 
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {

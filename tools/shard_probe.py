@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--layout", default="strided", choices=["strided", "contig"],
+                    help="contig: rank r renders one block of ceil(H/N) rows (coherence probe; unbalanced)")
     a = ap.parse_args()
     import torch
 
@@ -40,13 +42,16 @@ def main():
     H, W = lib.camera_resolve(cam).image_height, c["width"]
     ds = lib.scene_create(s.desc)
     stream = torch.cuda.current_stream().cuda_stream
-    res = {"config": a.config, "height": H, "width": W, "per_n": {}}
+    res = {"config": a.config, "layout": a.layout, "height": H, "width": W, "per_n": {}}
     full_ms = None
     for n in [int(x) for x in a.ns.split(",")]:
         out = torch.zeros((rtgpu.padded_rows(H, n), W, 3), device="cuda")
         kern, wall = [], []
         for r in range(n):
             b, stride, cnt = rtgpu.shard_rows(H, r, n)
+            if a.layout == "contig":
+                rows = rtgpu.padded_rows(H, n)
+                b, stride, cnt = r * rows, 1, max(0, min(rows, H - r * rows))
             best_k, best_w = 1e30, 1e30
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -59,7 +64,8 @@ def main():
             wall.append(round(best_w, 3))
         if full_ms is None:
             full_ms = max(wall)
-        res["per_n"][n] = {"kernel_ms": kern, "wall_ms": wall, "max_wall_ms": max(wall),
+        res["per_n"][n] = {"kernel_ms": kern, "sum_kernel_ms": round(sum(kern), 3), "wall_ms": wall,
+                           "max_wall_ms": max(wall),
                            "efficiency_vs_n1": round(full_ms / (n * max(wall)), 4)}
         print(json.dumps({n: res["per_n"][n]}), file=sys.stderr, flush=True)
     ds.close()

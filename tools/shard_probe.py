@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--lib", default="", help="librtgpu.so to load (default: the in-tree build)")
     ap.add_argument("--layout", default="strided", choices=["strided", "contig"],
                     help="contig: rank r renders one block of ceil(H/N) rows (coherence probe; unbalanced)")
     a = ap.parse_args()
@@ -34,7 +35,7 @@ def main():
     from bench import CONFIGS
 
     c = CONFIGS[a.config]
-    lib = rtgpu.Library()
+    lib = rtgpu.Library(a.lib or None)
     s = rtgpu.SceneLibrary().build(c["scene"], grid=c["grid"], image_width=c["width"],
                                    aspect_ratio=c["width"] / c["height"], spp=c["spp"],
                                    max_depth=c["depth"], rand_seed=1)
@@ -42,7 +43,7 @@ def main():
     H, W = lib.camera_resolve(cam).image_height, c["width"]
     ds = lib.scene_create(s.desc)
     stream = torch.cuda.current_stream().cuda_stream
-    res = {"config": a.config, "layout": a.layout, "height": H, "width": W, "per_n": {}}
+    res = {"config": a.config, "lib": a.lib or "default", "layout": a.layout, "height": H, "width": W, "per_n": {}}
     full_ms = None
     for n in [int(x) for x in a.ns.split(",")]:
         out = torch.zeros((rtgpu.padded_rows(H, n), W, 3), device="cuda")

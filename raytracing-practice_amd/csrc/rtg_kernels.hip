@@ -776,6 +776,10 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   return true;
 }
 
+// Wave ballot of a lane predicate straight from its condition mask (HIP's __ballot takes an int,
+// which makes the compiler materialise the predicate in a VGPR and compare it again).
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
@@ -902,7 +906,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   for (;;) {
     // hand the next units of the current batch (new batches as needed) to the lanes without one
-    uint64_t want = __ballot(!has);
+    uint64_t want = ballot(!has);
     while (want != 0 && !exhausted) {
       if (k_next >= 64) {
         int b = 0;
@@ -944,13 +948,13 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       k_next += take;
-      want = __ballot(!has);
+      want = ballot(!has);
     }
     if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
     if (fresh || cont) trav_begin(tr, S, ps.o, ps.d);
     fresh = false;
     cont = false;
-    const int alive = __popcll(__ballot(has));
+    const int alive = __popcll(ballot(has));
     if (alive == 0) break;
     const int need = (alive * J.shade_batch + 63) >> 6;
     uint64_t t_trav0 = 0;
@@ -958,11 +962,11 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     for (;;) {
       if (COUNT) {
         w.diag[0] += 1;
-        w.diag[1] += __popcll(__ballot(tr.active));
-        w.diag[2] += __popcll(__ballot(!has));
+        w.diag[1] += __popcll(ballot(tr.active));
+        w.diag[2] += __popcll(ballot(!has));
       }
-      const int at_leaf = __popcll(__ballot(tr.active && tr.todo < 0));
-      const bool inner_left = __ballot(tr.active && tr.todo >= 0) != 0;
+      const int at_leaf = __popcll(ballot(tr.active && tr.todo < 0));
+      const bool inner_left = ballot(tr.active && tr.todo >= 0) != 0;
       const bool leaf_trip = at_leaf >= J.leaf_batch || !inner_left;
       uint64_t tl = 0;
       if (COUNT) {
@@ -971,7 +975,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           w.diag[10] += at_leaf;
           tl = __builtin_amdgcn_s_memtime();
         } else {
-          w.diag[9] += __popcll(__ballot(tr.active && tr.todo >= 0));
+          w.diag[9] += __popcll(ballot(tr.active && tr.todo >= 0));
         }
       }
       if (leaf_trip && tr.active && tr.todo < 0)
@@ -985,8 +989,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
       }
       if (COUNT && leaf_trip) w.diag[8] += __builtin_amdgcn_s_memtime() - tl;
-      const uint64_t trav = __ballot(tr.active);
-      const int ready = __popcll(__ballot(!tr.active && has));
+      const uint64_t trav = ballot(tr.active);
+      const int ready = __popcll(ballot(!tr.active && has));
       if (trav == 0 || ready >= need) break;
     }
     uint64_t t_shade0 = 0;
@@ -994,7 +998,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       t_shade0 = __builtin_amdgcn_s_memtime();
       w.diag[5] += t_shade0 - t_trav0;
       w.diag[3] += 1;
-      w.diag[4] += __popcll(__ballot(!tr.active && has));
+      w.diag[4] += __popcll(ballot(!tr.active && has));
     }
     if (!tr.active && has) {
       ++w.segs;

@@ -188,6 +188,7 @@ def main():
     achieved = algo_bytes / avg_kernel_s / 1e9
     workload = (f"{args.scene}(grid={args.grid}) {W}x{H} {args.spp}spp depth{args.depth} bvh={args.bvh} "
                 f"chunk={rtgpu.chunk_samples(args.spp)}")
+    traffic = pmc_traffic(workload)
 
     if rank == 0:
         samples = W * H * args.spp * args.steps
@@ -211,7 +212,12 @@ def main():
                        "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather ({args.gather}) to rank 0"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(workload),
+                         "traffic": traffic,
+                         "traffic_gbs": (round(traffic / avg_kernel_s / 1e9, 2) if traffic else None),
+                         "note": ("frac > 1: the algorithmic bytes are served on chip (LDS-resident scene, "
+                                  "or L2/MALL for scenes too large for LDS); traffic = PMC-measured HBM bytes "
+                                  "per launch (null when not measured for this workload); the binding "
+                                  "resource is VALU issue and LDS/cache latency (DESIGN.md section 6)"),
                          "kernel_ms": round(avg_kernel_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(algo_bytes),
                          "per_segment": {"box_tests": round(cst.box_tests / cst.segments, 3),

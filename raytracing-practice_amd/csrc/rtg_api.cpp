@@ -231,8 +231,42 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     }
     bvh.refs.resize(d->num_prims);
     for (int64_t i = 0; i < d->num_prims; ++i) bvh.refs[i] = i;
-  } else if (!build_bvh(&bd, &bvh, err)) {
-    return false;
+  } else {
+    // 4-wide SAH trees: a sphere whose box covers at least half of the scene box's surface area
+    // (a ground sphere) is kept out of the tree; every ray tests it before traversing, so the leaf
+    // trips it would cost are gone and the traversal starts with its hit as the closest so far
+    int64_t occ = -1;
+    if (d->bvh_mode == RTG_BVH_SAH && d->num_prims > 1 && !std::getenv("RTG_NO_OCCLUDER")) {
+      double slo[3] = {1e300, 1e300, 1e300}, shi[3] = {-1e300, -1e300, -1e300};
+      std::vector<double> area(d->num_prims);
+      for (int64_t i = 0; i < d->num_prims; ++i) {
+        double lo[3], hi[3];
+        prim_bbox(d->prims[i], lo, hi);
+        for (int a = 0; a < 3; ++a) {
+          slo[a] = std::min(slo[a], lo[a]);
+          shi[a] = std::max(shi[a], hi[a]);
+        }
+        const double ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+        area[i] = ex * ey + ey * ez + ez * ex;
+      }
+      const double ex = shi[0] - slo[0], ey = shi[1] - slo[1], ez = shi[2] - slo[2];
+      const double scene_area = ex * ey + ey * ez + ez * ex;
+      for (int64_t i = 0; i < d->num_prims; ++i)
+        if (d->prims[i].kind == RTG_PRIM_SPHERE && area[i] >= 0.5 * scene_area && (occ < 0 || area[i] > area[occ]))
+          occ = i;
+    }
+    std::vector<rtg_primitive> rest;
+    if (occ >= 0) {
+      rest.reserve(d->num_prims - 1);
+      for (int64_t i = 0; i < d->num_prims; ++i)
+        if (i != occ) rest.push_back(d->prims[i]);
+      bd.prims = rest.data();
+      bd.num_prims = d->num_prims - 1;
+    }
+    if (!build_bvh(&bd, &bvh, err)) return false;
+    if (occ >= 0)  // refs back to input indices
+      for (auto& r : bvh.refs) r = r >= occ ? r + 1 : r;
+    out->occluder_prim = occ;
   }
   out->num_prims = d->num_prims;
   out->num_nodes = static_cast<int64_t>(bvh.nodes.size());
@@ -296,6 +330,15 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       }
     }
     out->refs[r] = (p.kind == RTG_PRIM_QUAD) ? (slot[pid] | kQuadRefBit) : slot[pid];
+  }
+  if (out->occluder_prim >= 0) {  // after every referenced sphere, so the refs stay the identity
+    const rtg_primitive& p = d->prims[out->occluder_prim];
+    out->occluder = nsph++;
+    const float rec[8] = {static_cast<float>(p.p0[0]),          static_cast<float>(p.p0[1]),
+                          static_cast<float>(p.p0[2]),          static_cast<float>(p.radius),
+                          static_cast<float>(p.p1[0] - p.p0[0]), static_cast<float>(p.p1[1] - p.p0[1]),
+                          static_cast<float>(p.p1[2] - p.p0[2]), ibits_to_float(p.material)};
+    out->spheres.insert(out->spheres.end(), rec, rec + 8);
   }
 
   // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
@@ -662,6 +705,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
   s->dev.num_nodes = hs.num_nodes;
   s->dev.root_code = 0;
+  s->dev.occluder = hs.occluder;
   s->dev.node_limit = static_cast<int32_t>(std::min<int64_t>(hs.num_nodes * 112, INT32_MAX));
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);

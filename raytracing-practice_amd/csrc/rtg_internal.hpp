@@ -42,6 +42,8 @@ struct HostScene {
   int32_t node_width = 2;  // 2: child-pair 64-B nodes, 4: 4-wide 112-B nodes
   int64_t num_prims = 0;
   bool gpu_bvh = false;       // RTG_BVH_GPU: nodes are built on the device after the upload
+  int64_t occluder_prim = -1;  // input primitive kept out of the BVH (a sphere; -1: none)
+  int32_t occluder = -1;       // its sphere index (stored after the BVH-referenced spheres)
   int64_t node_capacity = 0;  // gpu_bvh: 4-wide nodes to reserve
 };
 
@@ -130,6 +132,9 @@ struct DevScene {
   // valid one is below node_limit (root_code + num_nodes * 112)
   int32_t root_code;
   int32_t node_limit;
+  // a sphere whose box spans most of the scene (book-1's ground) is kept out of the BVH and tested
+  // by every ray before its traversal, in the shading phase (sphere index, -1: none)
+  int32_t occluder;
 };
 
 struct GpuBvhResult {  // rtg_gpubvh.hip

@@ -951,7 +951,18 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       want = ballot(!has);
     }
     if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
-    if (fresh || cont) trav_begin(tr, S, ps.o, ps.d);
+    if (fresh || cont) {
+      trav_begin(tr, S, ps.o, ps.d);
+      if (S.occluder >= 0) {  // the scene-spanning sphere kept out of the BVH (DevScene::occluder)
+        const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * 2;
+        if (COUNT) w.cnt.prim += 1;
+        const float th = sphere_t(sp4[0], sp4[1], ps.o, ps.d, ps.time, kTMin, tr.tbest);
+        if (th > 0.0f) {
+          tr.tbest = th;
+          tr.best = S.occluder;
+        }
+      }
+    }
     fresh = false;
     cont = false;
     const int alive = __popcll(ballot(has));

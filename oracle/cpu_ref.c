@@ -825,15 +825,21 @@ static void world32_free(world32* w) {
   free(w->pvec);
 }
 
-/* sphere::hit, fp32 robust form: returns root or -1 */
+/* sphere::hit, fp32 robust form: c = |oc|^2 - r^2 in f64 for |r| >= 16, fp32 below;
+   returns root or -1 */
 static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, float tmax) {
   f3 C = F3(s[0] + time * s[4], s[1] + time * s[5], s[2] + time * s[6]);
   f3 oc = fv_sub(o, C);
   float a = fdot(d, d);
   float hb = fdot(oc, d);
-  double ox = (double)o.x - (double)C.x, oy = (double)o.y - (double)C.y,
-         oz = (double)o.z - (double)C.z, r = (double)s[3];
-  float c = (float)((ox * ox + oy * oy + oz * oz) - r * r);
+  float c;
+  if (fabsf(s[3]) < 16.0f) {
+    c = fdot(oc, oc) - s[3] * s[3];
+  } else {
+    double ox = (double)o.x - (double)C.x, oy = (double)o.y - (double)C.y,
+           oz = (double)o.z - (double)C.z, r = (double)s[3];
+    c = (float)((ox * ox + oy * oy + oz * oz) - r * r);
+  }
   float disc = hb * hb - a * c;
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);

@@ -106,18 +106,26 @@ __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
 // ---------------------------------------------------------------------------------------
 // Geometry
 // sphere::hit (sphere.hpp:47-93) with the fp32-robust root form of DESIGN.md: c = |oc|^2 - r^2
-// is formed in f64, the near root as c/q. Returns the root or -1.
+// is formed in f64 for spheres of radius >= kSphereF64Radius (a ground sphere, where fp32
+// cancellation would put self-hits above tmin), in fp32 below it; the near root is c/q. Returns
+// the root or -1.
+constexpr float kSphereF64Radius = 16.0f;
 __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float time, float tmin,
                                           float tmax) {
   const V3 C = v3(s0.x + time * s1.x, s0.y + time * s1.y, s0.z + time * s1.z);
   const V3 oc = sub(o, C);
   const float a = dot(d, d);
   const float hb = dot(oc, d);
-  const double ox = static_cast<double>(o.x) - static_cast<double>(C.x);
-  const double oy = static_cast<double>(o.y) - static_cast<double>(C.y);
-  const double oz = static_cast<double>(o.z) - static_cast<double>(C.z);
-  const double r = static_cast<double>(s0.w);
-  const float c = static_cast<float>((ox * ox + oy * oy + oz * oz) - r * r);
+  float c;
+  if (fabsf(s0.w) < kSphereF64Radius) {
+    c = dot(oc, oc) - s0.w * s0.w;
+  } else {
+    const double ox = static_cast<double>(o.x) - static_cast<double>(C.x);
+    const double oy = static_cast<double>(o.y) - static_cast<double>(C.y);
+    const double oz = static_cast<double>(o.z) - static_cast<double>(C.z);
+    const double r = static_cast<double>(s0.w);
+    c = static_cast<float>((ox * ox + oy * oy + oz * oz) - r * r);
+  }
   const float disc = hb * hb - a * c;
   if (disc < 0.0f) return -1.0f;
   const float sq = sqrtf(disc);

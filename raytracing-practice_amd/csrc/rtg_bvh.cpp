@@ -150,7 +150,7 @@ struct Builder {
   // ---- binned SAH ----
   static constexpr int kBins = 16;
   int kMaxLeaf = 4;        // primitives per leaf (<= 8, the leaf code's count field)
-  double trav_cost = 0.7;  // cost of one more level relative to one primitive test (measured best)
+  double trav_cost = 0.5;  // cost of one more level relative to one primitive test (measured best)
 
   // Returns a child code for the range; `node_depth` = depth of the node that would own it.
   int32_t sah_child(int64_t start, int64_t end, const Box& bbox, int depth, int32_t* count) {

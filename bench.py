@@ -55,14 +55,15 @@ def parse():
                     help="gather the linear fp32 frame (default) or the write_color bytes (4x fewer)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-spp", type=int, default=None,
-                    help="spp of the bounded CPU sample (default 8; 2 for the 4K config 5)")
+                    help="spp of the bounded CPU sample (default 80, ~10 s on 16 cores; 10 for the 4K config 5)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
     if a.cpu_spp is None:
-        a.cpu_spp = 2 if a.width * a.height > 4_000_000 else 8
+        # about 10 s of CPU work on 16 host cores (the rate is spp-invariant)
+        a.cpu_spp = 10 if a.width * a.height > 4_000_000 else 80
     return a
 
 

@@ -15,7 +15,8 @@
  *
  *  orc_render_f32  ("cpu_ref32")  the fp32 spec the GPU implements (DESIGN.md "rtg-f32"):
  *                  counter RNG keyed by (seed, pixel, sample), iterative throughput form (H12),
- *                  robust sphere / quad roots with the plane/sphere offsets formed in f64. This is
+ *                  robust sphere / quad roots, the plane offset and a large sphere's (|r| >= 16)
+ *                  |oc|^2 - r^2 formed in f64. This is
  *                  the per-pixel parity target of the HIP kernels (same seeds => same pixels).
  *
  * Build: oracle/Makefile (gcc -O2 -ffp-contract=off, so expressions round as written).

@@ -32,11 +32,11 @@ constexpr int kMaxStackNeed = 4096;     // traversal stack entries per lane (LDS
 constexpr int kPlainWgsPerCu = 5;        // schedule 4 grid: resident workgroups per CU (waves pull work)
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
 constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
-// Scenes with a handful of BVH nodes (Cornell's 18 quads, earth + perlin's 2 spheres) reach their
-// leaves after one or two node steps, so waiting for more lanes there costs little and fills the
-// (expensive: quads, textures) leaf trips: Cornell -15 %, earth_perlin -1.5 % (profiles/r01_leafbatch)
+// Scenes with a handful of BVH nodes once waited for 48 lanes (Cornell -15 % with the SAH cost 0.7
+// tree, profiles/r01_leafbatch); with the cost 0.5 tree and the ground occluder 12 is as good or
+// better there too (Cornell 13.97 -> 13.56 ms at 800x450x300, earth_perlin 17.40 vs 17.43 ms)
 constexpr int kSmallBvhNodes = 16;
-constexpr int kSmallBvhLeafBatch = 48;
+constexpr int kSmallBvhLeafBatch = 12;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
 }

@@ -282,6 +282,30 @@ def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypat
     ds.close()
 
 
+@pytest.mark.parametrize("name", ["bouncing_spheres", "simple_light", "earth_perlin"])
+def test_occluder_changes_work_not_pixels(gpu_lib, scenes, monkeypatch, name):
+    """A scene-spanning sphere (the ground) is kept out of the SAH tree and tested by every ray
+    before its traversal (DESIGN.md §3 "Scene-spanning occluder"). The closest hit is the same
+    minimum either way, so the frame and the segment count must not change."""
+    frames, stats = [], []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("RTG_NO_OCCLUDER", "1")
+        else:
+            monkeypatch.delenv("RTG_NO_OCCLUDER", raising=False)
+        s = scenes.build(name, rand_seed=1)
+        c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+        c.image_width, c.samples_per_pixel, c.max_depth = 96, 8, 20
+        ds = gpu_lib.scene_create(s.desc)
+        img, st = ds.render_host(c)
+        ds.close()
+        frames.append(img)
+        stats.append(st)
+    same = float(np.mean(np.all(frames[0] == frames[1], axis=-1)))
+    assert same >= 0.999, same  # exact-t ties only (H9)
+    assert abs(int(stats[0].segments) - int(stats[1].segments)) <= 2
+
+
 @pytest.mark.parametrize("name,W", [("bouncing_spheres", 96), ("cornell_box", 64), ("simple_light", 64),
                                     ("quads", 48)])
 def test_device_bvh_build_matches_oracle(gpu_lib, scenes, oracle, name, W):

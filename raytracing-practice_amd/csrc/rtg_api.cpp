@@ -526,6 +526,15 @@ struct rtg_scene {
   DevScene dev{};
   rtg_scene_info info{};
   int stack_need = 0;  // structural maximum of traversal stack entries of the BVH
+  // host-output renders land in this pinned staging buffer first (DMA to pinned memory completes
+  // with the stream; an async copy straight into pageable user memory was seen to return from
+  // the stream sync before all of its bytes had arrived), then a host memcpy to the caller
+  void* host_stage = nullptr;
+  size_t host_stage_bytes = 0;
+  float* dev_out = nullptr;  // device frame of host-output renders (kept between renders)
+  size_t dev_out_bytes = 0;
+  float* pending_host_out = nullptr;
+  size_t pending_host_bytes = 0;
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
@@ -757,6 +766,8 @@ void rtg_scene_destroy(rtg_scene* s) {
   if (s->dmem) (void)hipFree(s->dmem);
   if (s->counters) (void)hipFree(s->counters);
   if (s->host_counters) (void)hipHostFree(s->host_counters);
+  if (s->host_stage) (void)hipHostFree(s->host_stage);
+  if (s->dev_out) (void)hipFree(s->dev_out);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
@@ -768,6 +779,10 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   float ms = 0.0f;
   RTG_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1), "hipEventElapsedTime");
   RTG_HIP(hipStreamSynchronize(s->pending_stream), "render stream");
+  if (s->pending_host_out) {
+    std::memcpy(s->pending_host_out, s->host_stage, s->pending_host_bytes);
+    s->pending_host_out = nullptr;
+  }
   const unsigned long long* c = s->host_counters;
   s->pending = false;
   if (stats) {
@@ -832,8 +847,16 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   hipStream_t stream = job->stream ? static_cast<hipStream_t>(job->stream) : s->own_stream;
   const size_t out_bytes = static_cast<size_t>(rows) * W * 3 * sizeof(float);
   float* dout = out_rgb;
-  if (!dev_out && out_rgb) {
-    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dout), out_bytes, stream), "hipMallocAsync(out)");
+  if (!dev_out && out_rgb) {  // a scene-owned device frame (not the stream-ordered pool)
+    if (s->dev_out_bytes < out_bytes) {
+      RTG_HIP(hipStreamSynchronize(stream), "stream sync");
+      if (s->dev_out) RTG_HIP(hipFree(s->dev_out), "hipFree(out)");
+      s->dev_out = nullptr;
+      s->dev_out_bytes = 0;
+      RTG_HIP(hipMalloc(reinterpret_cast<void**>(&s->dev_out), out_bytes), "hipMalloc(out)");
+      s->dev_out_bytes = out_bytes;
+    }
+    dout = s->dev_out;
   }
   DevJob dj{};
   dj.seed_mix = mix64(job->seed);
@@ -968,8 +991,16 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
                          hipMemcpyDeviceToHost, stream),
           "hipMemcpyAsync(counters)");
   if (!dev_out && out_rgb) {
-    RTG_HIP(hipMemcpyAsync(out_rgb, dout, out_bytes, hipMemcpyDeviceToHost, stream), "hipMemcpy(out)");
-    RTG_HIP(hipFreeAsync(dout, stream), "hipFreeAsync(out)");
+    if (s->host_stage_bytes < out_bytes) {
+      if (s->host_stage) RTG_HIP(hipHostFree(s->host_stage), "hipHostFree(stage)");
+      s->host_stage = nullptr;
+      s->host_stage_bytes = 0;
+      RTG_HIP(hipHostMalloc(&s->host_stage, out_bytes), "hipHostMalloc(stage)");
+      s->host_stage_bytes = out_bytes;
+    }
+    RTG_HIP(hipMemcpyAsync(s->host_stage, dout, out_bytes, hipMemcpyDeviceToHost, stream), "hipMemcpy(out)");
+    s->pending_host_out = out_rgb;
+    s->pending_host_bytes = out_bytes;
   }
   s->pending = true;
   s->pending_stream = stream;

@@ -121,6 +121,19 @@ def test_schedules_give_identical_frames(gpu_lib, scenes):
     assert max(segs) - min(segs) <= 2
 
 
+def test_repeated_host_renders_are_identical(gpu_lib, scenes):
+    """Host-output renders go through a scene-owned device frame and a pinned staging buffer; with
+    a stream-ordered (hipMallocAsync) frame the third render of a scene came back all zero."""
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 96, 4, 20
+    ds = gpu_lib.scene_create(s.desc)
+    frames = [ds.render_host(c, count=bool(k % 2))[0] for k in range(5)]
+    ds.close()
+    assert float(frames[0].sum()) > 0.0
+    assert all(np.array_equal(f, frames[0]) for f in frames[1:])
+
+
 def test_shards_and_determinism(gpu_lib, scenes):
     s = scenes.build("bouncing_spheres", rand_seed=1)
     c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)

@@ -833,15 +833,19 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   f3 oc = fv_sub(o, C);
   float a = fdot(d, d);
   float hb = fdot(oc, d);
-  float c;
+  float c, disc;
   if (fabsf(s[3]) < 16.0f) {
+    /* disc = a (r^2 - |oc - (h/a) d|^2), 1/a rounded first */
     c = fdot(oc, oc) - s[3] * s[3];
+    float inv_a = 1.0f / a, sh = hb * inv_a;
+    f3 f = F3(oc.x - sh * d.x, oc.y - sh * d.y, oc.z - sh * d.z);
+    disc = a * (s[3] * s[3] - fdot(f, f));
   } else {
     double ox = (double)o.x - (double)C.x, oy = (double)o.y - (double)C.y,
            oz = (double)o.z - (double)C.z, r = (double)s[3];
     c = (float)((ox * ox + oy * oy + oz * oz) - r * r);
+    disc = hb * hb - a * c;
   }
-  float disc = hb * hb - a * c;
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);
   float q = -(hb + copysignf(sq, hb));

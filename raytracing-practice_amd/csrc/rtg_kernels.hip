@@ -107,8 +107,8 @@ __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
 // Geometry
 // sphere::hit (sphere.hpp:47-93) with the fp32-robust root form of DESIGN.md: c = |oc|^2 - r^2
 // is formed in f64 for spheres of radius >= kSphereF64Radius (a ground sphere, where fp32
-// cancellation would put self-hits above tmin), in fp32 below it; the near root is c/q. Returns
-// the root or -1.
+// cancellation would put self-hits above tmin), in fp32 below it, where the discriminant is
+// taken from the centre-to-line distance; the near root is c/q. Returns the root or -1.
 constexpr float kSphereF64Radius = 16.0f;
 __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float time, float tmin,
                                           float tmax) {
@@ -116,17 +116,24 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const V3 oc = sub(o, C);
   const float a = dot(d, d);
   const float hb = dot(oc, d);
-  float c;
+  float c, disc;
   if (fabsf(s0.w) < kSphereF64Radius) {
     c = dot(oc, oc) - s0.w * s0.w;
+    // disc = a (r^2 - |f|^2), f = oc - (h/a) d the centre-to-line offset: no h^2 - a c
+    // cancellation, so a grazing ray far from a small sphere is classified to ~r^2 2^-22, not
+    // ~h^2 2^-24 (a false hit outside the sphere's box, which box culling precision then decides)
+    const float inv_a = 1.0f / a;
+    const float s = hb * inv_a;
+    const V3 f = v3(oc.x - s * d.x, oc.y - s * d.y, oc.z - s * d.z);
+    disc = a * (s0.w * s0.w - dot(f, f));
   } else {
     const double ox = static_cast<double>(o.x) - static_cast<double>(C.x);
     const double oy = static_cast<double>(o.y) - static_cast<double>(C.y);
     const double oz = static_cast<double>(o.z) - static_cast<double>(C.z);
     const double r = static_cast<double>(s0.w);
     c = static_cast<float>((ox * ox + oy * oy + oz * oz) - r * r);
+    disc = hb * hb - a * c;
   }
-  const float disc = hb * hb - a * c;
   if (disc < 0.0f) return -1.0f;
   const float sq = sqrtf(disc);
   const float q = -(hb + copysignf(sq, hb));

@@ -344,8 +344,10 @@ def test_device_bvh_build_million_spheres(gpu_lib, scenes, oracle):
 
 
 def test_million_sphere_scene(gpu_lib, scenes, oracle):
-    """BASELINE config 5 scene (grid 500 -> 1,000,001 objects, deep BVH) at a small image."""
-    g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", grid=500, image_width=64,
+    """BASELINE config 5 scene (grid 500 -> 1,000,001 objects, deep BVH) at a small image. 192 px
+    wide: enough far-away grazing rays that the old h^2 - a c discriminant made the frame depend
+    on box-culling precision (0.03 % of the pixels at 384 px)."""
+    g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", grid=500, image_width=192,
                              aspect_ratio=16.0 / 9.0, samples_per_pixel=2, max_depth=50)
     assert_parity(g, o, st, segs)
 

@@ -224,37 +224,40 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   if (binary_sah) bd.bvh_mode = RTG_BVH_SAH;
   const bool gpu_bvh = d->bvh_mode == RTG_BVH_GPU;
   Bvh bvh;
+  // 4-wide trees (host SAH or device-built): a sphere whose box covers at least half of the scene
+  // box's surface area (a ground sphere) is kept out of the tree; every ray tests it before
+  // traversing, so the leaf trips it would cost are gone and the traversal starts with its hit as
+  // the closest so far
+  int64_t occ = -1;
+  if ((d->bvh_mode == RTG_BVH_SAH || gpu_bvh) && d->num_prims > 1 && !std::getenv("RTG_NO_OCCLUDER")) {
+    double slo[3] = {1e300, 1e300, 1e300}, shi[3] = {-1e300, -1e300, -1e300};
+    std::vector<double> area(d->num_prims);
+    for (int64_t i = 0; i < d->num_prims; ++i) {
+      double lo[3], hi[3];
+      prim_bbox(d->prims[i], lo, hi);
+      for (int a = 0; a < 3; ++a) {
+        slo[a] = std::min(slo[a], lo[a]);
+        shi[a] = std::max(shi[a], hi[a]);
+      }
+      const double ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+      area[i] = ex * ey + ey * ez + ez * ex;
+    }
+    const double ex = shi[0] - slo[0], ey = shi[1] - slo[1], ez = shi[2] - slo[2];
+    const double scene_area = ex * ey + ey * ez + ez * ex;
+    for (int64_t i = 0; i < d->num_prims; ++i)
+      if (d->prims[i].kind == RTG_PRIM_SPHERE && area[i] >= 0.5 * scene_area && (occ < 0 || area[i] > area[occ]))
+        occ = i;
+  }
+  out->occluder_prim = occ;
   if (gpu_bvh) {  // primitives in input order; the device builds the tree (rtg_gpubvh.hip)
     if (d->num_prims > (int64_t(1) << 28) || d->num_prims > INT32_MAX / 112) {
       *err = "too many primitives for the device BVH builder";
       return false;
     }
-    bvh.refs.resize(d->num_prims);
-    for (int64_t i = 0; i < d->num_prims; ++i) bvh.refs[i] = i;
+    bvh.refs.reserve(d->num_prims);
+    for (int64_t i = 0; i < d->num_prims; ++i)
+      if (i != occ) bvh.refs.push_back(i);
   } else {
-    // 4-wide SAH trees: a sphere whose box covers at least half of the scene box's surface area
-    // (a ground sphere) is kept out of the tree; every ray tests it before traversing, so the leaf
-    // trips it would cost are gone and the traversal starts with its hit as the closest so far
-    int64_t occ = -1;
-    if (d->bvh_mode == RTG_BVH_SAH && d->num_prims > 1 && !std::getenv("RTG_NO_OCCLUDER")) {
-      double slo[3] = {1e300, 1e300, 1e300}, shi[3] = {-1e300, -1e300, -1e300};
-      std::vector<double> area(d->num_prims);
-      for (int64_t i = 0; i < d->num_prims; ++i) {
-        double lo[3], hi[3];
-        prim_bbox(d->prims[i], lo, hi);
-        for (int a = 0; a < 3; ++a) {
-          slo[a] = std::min(slo[a], lo[a]);
-          shi[a] = std::max(shi[a], hi[a]);
-        }
-        const double ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
-        area[i] = ex * ey + ey * ez + ez * ex;
-      }
-      const double ex = shi[0] - slo[0], ey = shi[1] - slo[1], ez = shi[2] - slo[2];
-      const double scene_area = ex * ey + ey * ez + ez * ex;
-      for (int64_t i = 0; i < d->num_prims; ++i)
-        if (d->prims[i].kind == RTG_PRIM_SPHERE && area[i] >= 0.5 * scene_area && (occ < 0 || area[i] > area[occ]))
-          occ = i;
-    }
     std::vector<rtg_primitive> rest;
     if (occ >= 0) {
       rest.reserve(d->num_prims - 1);
@@ -266,7 +269,6 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     if (!build_bvh(&bd, &bvh, err)) return false;
     if (occ >= 0)  // refs back to input indices
       for (auto& r : bvh.refs) r = r >= occ ? r + 1 : r;
-    out->occluder_prim = occ;
   }
   out->num_prims = d->num_prims;
   out->num_nodes = static_cast<int64_t>(bvh.nodes.size());
@@ -277,7 +279,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   if (gpu_bvh) {
     out->gpu_bvh = true;
     out->node_width = 4;
-    out->node_capacity = std::max<int64_t>(1, d->num_prims);
+    out->node_capacity = std::max<int64_t>(1, static_cast<int64_t>(bvh.refs.size()));
     out->num_nodes = 0;
     out->depth = 0;
     out->stack_need = 0;
@@ -681,17 +683,18 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     return cleanup(hip_fail(e, "hipStreamSynchronize(upload)"));
   const auto t2 = std::chrono::steady_clock::now();
   double gpu_build_ms = 0.0;
-  if (hs.gpu_bvh && hs.num_prims > 0) {  // RTG_BVH_GPU: build the nodes and leaf-ordered refs here
+  const int64_t nrefs = static_cast<int64_t>(hs.refs.size());
+  if (hs.gpu_bvh && nrefs > 0) {  // RTG_BVH_GPU: build the nodes and leaf-ordered refs here
     int32_t* refs_dev = reinterpret_cast<int32_t*>(base + parts[1].off);
     int32_t* sorted = nullptr;
-    if ((e = hipMallocAsync(reinterpret_cast<void**>(&sorted), hs.num_prims * 4, s->own_stream)) != hipSuccess)
+    if ((e = hipMallocAsync(reinterpret_cast<void**>(&sorted), nrefs * 4, s->own_stream)) != hipSuccess)
       return cleanup(hip_fail(e, "hipMalloc(bvh refs)"));
     GpuBvhResult r{};
     e = gpu_build_bvh4(reinterpret_cast<const float4*>(base + parts[2].off),
-                       reinterpret_cast<const float4*>(base + parts[3].off), refs_dev, hs.num_prims,
+                       reinterpret_cast<const float4*>(base + parts[3].off), refs_dev, nrefs,
                        reinterpret_cast<float*>(base + parts[0].off), hs.node_capacity, sorted, &r, s->own_stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(refs_dev, sorted, hs.num_prims * 4, hipMemcpyDeviceToDevice, s->own_stream);
+      e = hipMemcpyAsync(refs_dev, sorted, nrefs * 4, hipMemcpyDeviceToDevice, s->own_stream);
     const hipError_t ef = hipFreeAsync(sorted, s->own_stream);
     if (e == hipSuccess) e = ef;
     if (e == hipSuccess) e = hipStreamSynchronize(s->own_stream);

@@ -121,10 +121,14 @@ __global__ void morton_kernel(const Box6* boxes, int64_t n, const uint32_t* cbou
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Box6 b = boxes[i];
+  // one scale for all three axes (the centroid bounds' largest extent): per-axis scales give a
+  // thin axis — the 0.8-unit height of a 1000-unit sphere field — a third of the Morton bits, and
+  // every split on it leaves two children that each span the whole field (3.4x the box tests)
+  float ext = 0.0f;
+  for (int k = 0; k < 3; ++k) ext = fmaxf(ext, o2f(cbounds[3 + k]) - o2f(cbounds[k]));
   uint32_t q[3];
   for (int k = 0; k < 3; ++k) {
-    const float lo = o2f(cbounds[k]), hi = o2f(cbounds[3 + k]);
-    const float ext = hi - lo;
+    const float lo = o2f(cbounds[k]);
     const float c = 0.5f * (b.lo[k] + b.hi[k]);
     const float t = ext > 0.0f ? (c - lo) / ext : 0.5f;
     q[k] = static_cast<uint32_t>(fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f));

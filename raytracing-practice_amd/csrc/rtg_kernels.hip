@@ -1426,7 +1426,8 @@ hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J,
   if (variant == 3 || variant == 0)
     return S.node_width == 4 ? launch_default<4>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream)
                              : launch_default<2>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream);
-  if (S.node_width != 2) return hipErrorInvalidValue;  // schedules 1 and 2 traverse binary nodes only
+  // schedules 1 and 2 traverse binary nodes only, without a scene-spanning occluder
+  if (S.node_width != 2 || S.occluder >= 0) return hipErrorInvalidValue;
   switch (stack) {
     case 16:
       return launch_legacy<16>(S, C, J, count, variant, stream);

@@ -295,18 +295,20 @@ def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypat
     ds.close()
 
 
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU])
 @pytest.mark.parametrize("name", ["bouncing_spheres", "simple_light", "earth_perlin"])
-def test_occluder_changes_work_not_pixels(gpu_lib, scenes, monkeypatch, name):
-    """A scene-spanning sphere (the ground) is kept out of the SAH tree and tested by every ray
-    before its traversal (DESIGN.md §3 "Scene-spanning occluder"). The closest hit is the same
-    minimum either way, so the frame and the segment count must not change."""
+def test_occluder_changes_work_not_pixels(gpu_lib, scenes, monkeypatch, name, bvh):
+    """A scene-spanning sphere (the ground) is kept out of the 4-wide tree (host SAH or
+    device-built) and tested by every ray before its traversal (DESIGN.md §3 "Scene-spanning
+    occluder"). The closest hit is the same minimum either way, so the frame and the segment count
+    must not change."""
     frames, stats = [], []
     for off in (False, True):
         if off:
             monkeypatch.setenv("RTG_NO_OCCLUDER", "1")
         else:
             monkeypatch.delenv("RTG_NO_OCCLUDER", raising=False)
-        s = scenes.build(name, rand_seed=1)
+        s = scenes.build(name, rand_seed=1, bvh_mode=bvh)
         c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
         c.image_width, c.samples_per_pixel, c.max_depth = 96, 8, 20
         ds = gpu_lib.scene_create(s.desc)

@@ -1166,6 +1166,11 @@ int orc_kat_sphere_hit(const rtg_primitive* p, const double o[3], const double d
   }
   return h;
 }
+/* the rtg-f32 sphere test (sphere_t32) on one record {center, r, motion, material}: t or -1 */
+float orc_sphere_t32(const float s[8], const float o[3], const float d[3], float time, float tmin,
+                     float tmax) {
+  return sphere_t32(s, F3(o[0], o[1], o[2]), F3(d[0], d[1], d[2]), time, tmin, tmax);
+}
 int orc_kat_quad_hit(const rtg_primitive* p, const double o[3], const double d[3], double tmin,
                      double tmax, double rec[10], double bbox[6]) {
   rtg_scene_desc s;

@@ -49,6 +49,9 @@ class Oracle:
         L.orc_bvh_replay.restype = C.c_int64
         L.orc_sincos_turn.argtypes = [C.c_float, P(C.c_float), P(C.c_float)]
         L.orc_f32_unit_vector.argtypes = [C.c_uint64, P(C.c_float)]
+        L.orc_sphere_t32.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, C.c_float,
+                                     C.c_float]
+        L.orc_sphere_t32.restype = C.c_float
 
     def sincos_turn(self, u):
         sn, cs = C.c_float(), C.c_float()
@@ -114,6 +117,10 @@ class Oracle:
         rec = (C.c_double * 10)()
         h = self.lib.orc_kat_sphere_hit(C.byref(prim), self._d(o), self._d(d), time, tmin, tmax, rec)
         return bool(h), list(rec)
+
+    def sphere_t32(self, rec8, o, d, time=0.0, tmin=0.001, tmax=float("inf")):
+        f3 = C.c_float * 3
+        return float(self.lib.orc_sphere_t32((C.c_float * 8)(*rec8), f3(*o), f3(*d), time, tmin, tmax))
 
     def quad_hit(self, prim, o, d, tmin, tmax):
         rec, bbox = (C.c_double * 10)(), (C.c_double * 6)()

@@ -99,3 +99,48 @@ def test_direct_sampling_is_accurate_and_uniform(oracle):
     assert np.all(np.abs(norms - 1.0) < 1e-6)
     assert np.all(np.abs(v.mean(axis=0)) < 0.02)  # 3 sigma of 1/sqrt(3*20000) ~ 0.012
     assert np.allclose((v ** 2).mean(axis=0), 1.0 / 3.0, atol=0.01)
+
+
+def test_sphere_t32_grazing_far_spheres(oracle):
+    """rtg-f32 sphere test on grazing rays: a 0.2-radius sphere 50-1000 units from the
+    ray origin (the 1M-sphere field), the ray passing at r·(1 ± δ), δ ≤ 2e-3. Hit/miss must agree with
+    the exact (f64) classification of the same fp32 inputs whenever |δ| > 5e-4; the old discriminant
+    h² − a·c (emulated here in fp32, one rounding per operation) gets about half of them wrong
+    (1133 of 2295: a coin flip), the new form none."""
+    rng = np.random.default_rng(7)
+    f = np.float32
+    bad_new = bad_old = checked = 0
+    for _ in range(3000):
+        o = rng.uniform(-15, 15, 3).astype(f)
+        dist = rng.uniform(50, 1000)
+        u = rng.normal(size=3)
+        u /= np.linalg.norm(u)
+        C = (o + dist * u).astype(f)
+        r = f(0.2)
+        v = rng.normal(size=3)
+        v -= v.dot(u) * u
+        v /= np.linalg.norm(v)
+        delta = rng.uniform(-2e-3, 2e-3)
+        target = C.astype(np.float64) + float(r) * (1 + delta) * v
+        d = ((target - o) * rng.uniform(0.01, 0.2)).astype(f)
+        # exact classification of the fp32 inputs
+        O, D, Cd = o.astype(np.float64), d.astype(np.float64), C.astype(np.float64)
+        oc = O - Cd
+        s = -oc.dot(D) / D.dot(D)
+        miss = np.linalg.norm(oc + s * D)
+        rel = miss / float(r) - 1.0
+        if abs(rel) <= 5e-4 or s <= 0:
+            continue
+        checked += 1
+        exact_hit = rel < 0
+        t = oracle.sphere_t32([C[0], C[1], C[2], r, 0, 0, 0, 0], o, d)
+        bad_new += (t > 0) != exact_hit
+        # the old form: disc = h*h - a*c, every operation rounded to fp32
+        ocf = (o - C).astype(f)
+        a = f(f(f(d[0] * d[0]) + f(d[1] * d[1])) + f(d[2] * d[2]))
+        h = f(f(f(ocf[0] * d[0]) + f(ocf[1] * d[1])) + f(ocf[2] * d[2]))
+        c = f(f(f(f(ocf[0] * ocf[0]) + f(ocf[1] * ocf[1])) + f(ocf[2] * ocf[2])) - f(r * r))
+        bad_old += (f(f(h * h) - f(a * c)) >= 0) != exact_hit
+    assert checked > 2000
+    assert bad_new == 0, (bad_new, checked)
+    assert bad_old > 0.3 * checked, (bad_old, checked)

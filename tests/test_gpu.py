@@ -270,6 +270,28 @@ def test_empty_world_and_single_sphere(gpu_lib, oracle):
     assert_parity(g, o, st, segs)
 
 
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
+def test_ground_and_one_sphere(gpu_lib, oracle, bvh):
+    """A ground sphere and one small sphere: the ground becomes the scene-spanning occluder in the
+    4-wide modes, leaving a one-primitive tree (the device builder's n = 1 case)."""
+    cam = rtgpu.camera(image_width=32, aspect_ratio=1.5, samples_per_pixel=4, max_depth=8,
+                       background=(0.7, 0.8, 1.0), lookfrom=(0, 1, 4), lookat=(0, 0.5, 0))
+    tex = rtgpu.rtg_texture(type=rtgpu.RTG_TEX_SOLID, color=rtgpu.D3(0.5, 0.2, 0.1))
+    mat = rtgpu.rtg_material(type=rtgpu.RTG_MAT_LAMBERTIAN, texture=0)
+    ground = rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_SPHERE, material=0, p0=rtgpu.D3(0, -1000, 0),
+                                 p1=rtgpu.D3(0, -1000, 0), radius=1000.0)
+    ball = rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_SPHERE, material=0, p0=rtgpu.D3(0, 0.5, 0),
+                               p1=rtgpu.D3(0, 0.5, 0), radius=0.5)
+    d = _desc([ground, ball], [mat], [tex])
+    d.bvh_mode = bvh
+    ds = gpu_lib.scene_create(d)
+    g, st = ds.render_host(cam)
+    ds.close()
+    o, segs = oracle.render_f32(d, cam)
+    assert_parity(g, o, st, segs)
+    assert st.segments > 32 * 21 * 4  # rays bounce between the ball and the ground
+
+
 def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypatch):
     """Deep BVHs keep the first stack entries in LDS and the rest in a global per-wave spill area
     (the 1M-sphere scene needs 36 entries). RTG_STACK_LDS_ENTRIES lowers the LDS part so that the

@@ -54,39 +54,59 @@ def parse():
     ap.add_argument("--gather", choices=["f32", "rgb8"], default="f32",
                     help="gather the linear fp32 frame (default) or the write_color bytes (4x fewer)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-spp", type=int, default=None,
-                    help="spp of the bounded CPU sample (default 80, ~10 s on 16 cores; 10 for the 4K config 5)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="wall time the all-cores CPU sample is sized for (the 1-core sample adds ~3-5 s)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core of the host (cgroup quota bound)")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
-    if a.cpu_spp is None:
-        # about 10 s of CPU work on 16 host cores (the rate is spp-invariant)
-        a.cpu_spp = 10 if a.width * a.height > 4_000_000 else 80
     return a
 
 
-def cpu_baseline(args, scene_desc, cam):
-    """The reference timed on this host's cores: oracle/_ref/ref_harness (reference geometry,
-    BVH, RNG and vector code compiled from /root/reference; camera/material loop restated, see
-    DESIGN.md 'ref-hybrid') if it was built, else the oracle's fp64 port (cpu_ref64)."""
-    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    threads = args.cpu_threads or min(int(os.environ.get("OMP_NUM_THREADS", "16")), avail, 16)
-    W, H, spp, depth = args.width, args.height, args.cpu_spp, args.depth
-    sample = f"{args.scene} {W}x{H}, {spp} spp, depth {depth}, rows dealt over {threads} workers"
+def host_cpus():
+    """(cores this process may run on, CPU model, online CPUs, cgroup CPU quota or None). The cores
+    used are the affinity set, bounded by a cgroup CPU quota when one is set (more workers than the
+    quota would only time-share the same cores)."""
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    cores = avail if quota is None else max(1, min(avail, int(quota)))
+    return cores, model, os.cpu_count(), quota
+
+
+# scenes the ref-hybrid harness builds from the reference's own geometry code
+HARNESS_SCENE = {("bouncing_spheres", 11): "book1", ("cornell_box", 0): "cornell",
+                 ("bouncing_spheres", 500): "book1_g500"}
+
+
+def _cpu_run(args, scene_desc, cam, procs, spp, row_step):
+    """One timed CPU render of the workload's frame (rows 0, row_step, ... dealt over procs
+    workers, spp samples per pixel): (seconds, segments, kind, what)."""
+    W, H, depth = args.width, args.height, args.depth
     harness = os.path.join(REPO, "oracle", "_ref", "ref_harness")
-    # scenes the ref-hybrid harness builds from the reference's own geometry code
-    hscene = {("bouncing_spheres", 11): "book1", ("cornell_box", 0): "cornell"}.get((args.scene, args.grid))
+    hscene = HARNESS_SCENE.get((args.scene, args.grid))
     if hscene and os.access(harness, os.X_OK):
         try:
-            out = subprocess.run([harness, "bench", hscene, str(W), str(H), str(spp), str(depth),
-                                  str(threads)], check=True, capture_output=True, text=True,
-                                 timeout=600).stdout
+            out = subprocess.run([harness, "bench", hscene, str(W), str(H), str(spp), str(depth), str(procs),
+                                  str(row_step)], check=True, capture_output=True, text=True, timeout=900).stdout
             r = json.loads(out)
-            return {"value": round(r["mrays_per_s"], 3), "unit": "Mrays/s", "cores": threads,
-                    "kind": "reference", "sample": sample + " (ref-hybrid build)",
-                    "seconds": round(r["seconds"], 3), "segments": r["segments"]}
+            return r["seconds"], r["segments"], "reference", "ref-hybrid build"
         except (subprocess.SubprocessError, OSError, ValueError, KeyError) as e:
             print(f"[bench] ref_harness failed ({e}); timing the fp64 port instead", file=sys.stderr)
     import rtgpu
@@ -94,9 +114,40 @@ def cpu_baseline(args, scene_desc, cam):
 
     c = rtgpu.rtg_camera_desc.from_buffer_copy(cam)
     c.samples_per_pixel = spp
-    sec, segs = Oracle().bench_f64(scene_desc, c, threads, H)
-    return {"value": round(segs / sec / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": sample + " (cpu_ref64)", "seconds": round(sec, 3), "segments": segs}
+    sec, segs = Oracle().bench_f64(scene_desc, c, procs, H, row_step=row_step)
+    return sec, segs, "port", "cpu_ref64"
+
+
+def cpu_baseline(args, scene_desc, cam):
+    """The reference timed on this host's cores: oracle/_ref/ref_harness (reference
+    geometry, BVH, RNG and vector code compiled from /root/reference; camera/material loop
+    restated, DESIGN.md 'ref-hybrid') if it was built, else the oracle's fp64 port (cpu_ref64).
+    First one core on a row sample (~4 s, also the calibration), then every core of the host
+    (bounded by the cgroup quota) for ~cpu_seconds on the whole frame. The rate is spp-invariant."""
+    cores, model, online, quota = host_cpus()
+    threads = args.cpu_threads or cores
+    W, H = args.width, args.height
+    # 1 core: every row_step-th row (~68 rows), spp grown until the sample takes >= 2.5 s
+    step1, spp1 = max(1, H // 68), 1
+    while True:
+        sec1, segs1, kind, what = _cpu_run(args, scene_desc, cam, 1, spp1, step1)
+        if sec1 >= 2.5 or spp1 >= 64:
+            break
+        spp1 = min(64, max(spp1 + 1, int(spp1 * 3.0 / max(sec1, 1e-3))))
+    rate1 = segs1 / sec1
+    rows1 = len(range(0, H, step1))
+    rps = segs1 / (W * rows1 * spp1)  # segments per sample
+    # all cores: the whole frame, spp sized for ~cpu_seconds of wall time at threads x rate1
+    spp_all = max(1, int(round(args.cpu_seconds * rate1 * threads / (W * H * rps))))
+    sec, segs, kind, what = _cpu_run(args, scene_desc, cam, threads, spp_all, 1)
+    return {"value": round(segs / sec / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": kind,
+            "sample": f"{args.scene} {W}x{H}, {spp_all} spp, depth {args.depth}, rows dealt over {threads} "
+                      f"worker processes ({what})",
+            "seconds": round(sec, 3), "segments": segs,
+            "cpu_model": model, "host_cpus_online": online, "cgroup_cpu_quota": quota,
+            "one_core": {"value": round(rate1 / 1e6, 3), "unit": "Mrays/s", "seconds": round(sec1, 3),
+                         "segments": segs1,
+                         "sample": f"{rows1} rows (every {step1}th), {spp1} spp, 1 process ({what})"}}
 
 
 def pmc_traffic(workload):
@@ -149,8 +200,9 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     def step(i):
-        st = ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + i, row_begin=b,
-                              row_stride=stride, row_count=n)
+        # a rank past the image's last row renders nothing (its shard stays zero padding)
+        st = (ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + i, row_begin=b,
+                               row_stride=stride, row_count=n) if n > 0 else rtgpu.rtg_render_stats())
         if shard8 is not None:  # write_color on the device (rtg_resolve_rgb8), gather the bytes
             ds.resolve_rgb8(shard.data_ptr(), shard8.data_ptr(), shard.shape[0] * W, stream)
         if world > 1:
@@ -181,11 +233,11 @@ def main():
     total_segs, wall = float(tot.item()), float(tmax.item())
 
     # algorithmic bytes of one launch (counting variant of the same kernel, same seed, untimed)
-    cst = ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + args.warmup, row_begin=b,
-                           row_stride=stride, row_count=n, count=True)
+    cst = (ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + args.warmup, row_begin=b,
+                            row_stride=stride, row_count=n, count=True) if n > 0 else rtgpu.rtg_render_stats())
     algo_bytes = (BYTES_PER_BOX * cst.box_tests + BYTES_PER_PRIM * cst.prim_tests
                   + BYTES_PER_HIT * cst.hits)
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    avg_kernel_s = max(sum(kernel_ms) / len(kernel_ms) / 1e3, 1e-9)
     achieved = algo_bytes / avg_kernel_s / 1e9
     workload = (f"{args.scene}(grid={args.grid}) {W}x{H} {args.spp}spp depth{args.depth} bvh={args.bvh} "
                 f"chunk={rtgpu.chunk_samples(args.spp)}")
@@ -210,7 +262,9 @@ def main():
             "config": {"workload": workload, "baseline_config": args.config, "scene": args.scene,
                        "grid": args.grid, "width": W,
                        "height": H, "spp": args.spp, "depth": args.depth, "bvh": args.bvh,
-                       "parallelism": f"rows interleaved over {world} GPU(s), RCCL gather ({args.gather}) to rank 0"},
+                       "parallelism": (f"rows interleaved over {world} GPUs, one RCCL gather ({args.gather}) of the "
+                                       f"frame to rank 0 per step" if world > 1 else
+                                       "1 GPU, whole frame (no gather)")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
@@ -221,9 +275,9 @@ def main():
                                   "resource is VALU issue and LDS/cache latency (DESIGN.md section 6)"),
                          "kernel_ms": round(avg_kernel_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(algo_bytes),
-                         "per_segment": {"box_tests": round(cst.box_tests / cst.segments, 3),
-                                         "prim_tests": round(cst.prim_tests / cst.segments, 3),
-                                         "hit_frac": round(cst.hits / cst.segments, 4)}},
+                         "per_segment": {"box_tests": round(cst.box_tests / max(cst.segments, 1), 3),
+                                         "prim_tests": round(cst.prim_tests / max(cst.segments, 1), 3),
+                                         "hit_frac": round(cst.hits / max(cst.segments, 1), 4)}},
             "msamples_per_s": round(samples / wall / 1e6, 3),
             "rays_per_sample": round(total_segs / samples, 4),
             "scene_build_ms": round(t_scene * 1e3, 1),
@@ -233,8 +287,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, s.desc, cam)
-            cb = line["cpu_baseline"]["value"]
-            line["speedup_vs_cpu"] = round(line["value"] / cb, 1) if cb else None
+            cb = line["cpu_baseline"]
+            line["speedup_vs_cpu"] = round(line["value"] / cb["value"], 1) if cb["value"] else None
+            line["speedup_vs_cpu_one_core"] = (round(line["value"] / cb["one_core"]["value"], 1)
+                                               if cb["one_core"]["value"] else None)
         print(json.dumps(line), flush=True)
     ds.close()
     if world > 1:

@@ -593,7 +593,7 @@ typedef struct {
   const world64* w;
   const rtg_camera_desc* cam;
   unsigned seed;
-  int worker, workers, rows;
+  int worker, workers, rows, row_step;
   uint64_t segments;
 } bench_arg;
 static void* bench_worker(void* p) {
@@ -608,13 +608,14 @@ static void* bench_worker(void* p) {
   c.bg = dv(a->cam->background);
   c.g = &g;
   double* row = (double*)malloc(sizeof(double) * 3 * c.cp.image_width);
-  for (int j = a->worker; j < a->rows; j += a->workers) render64_rows(&c, j, 1, row);
+  for (int j = a->worker * a->row_step; j < a->rows; j += a->workers * a->row_step) render64_rows(&c, j, 1, row);
   free(row);
   a->segments = c.segments;
   return 0;
 }
-int orc_bench_f64(const rtg_scene_desc* s, const rtg_camera_desc* cam, int threads, int rows,
+int orc_bench_f64(const rtg_scene_desc* s, const rtg_camera_desc* cam, int threads, int rows, int row_step,
                   unsigned base_seed, double* seconds, uint64_t* segments) {
+  if (row_step < 1) row_step = 1;
   world64 w;
   world64_init(&w, s);
   if (threads < 1) threads = 1;
@@ -629,6 +630,7 @@ int orc_bench_f64(const rtg_scene_desc* s, const rtg_camera_desc* cam, int threa
     args[k].worker = k;
     args[k].workers = threads;
     args[k].rows = rows;
+    args[k].row_step = row_step;
     pthread_create(&th[k], 0, bench_worker, &args[k]);
   }
   uint64_t total = 0;
@@ -827,8 +829,12 @@ static void world32_free(world32* w) {
 }
 
 /* sphere::hit, fp32 robust form: c = |oc|^2 - r^2 in f64 for |r| >= 16, fp32 below;
-   returns root or -1 */
-static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, float tmax) {
+   returns root or -1. `origin`: the ray starts on this sphere (its previous segment hit it), so
+   the root at t ~ 0 is the ray's own origin and only the far root counts, and only for a ray
+   entering the sphere (h < 0) — DESIGN.md §4 "origin rule". In fp32 the origin lies ~ulp(|p|)
+   off the surface, and a grazing ray's own root c/q can exceed tmin = 0.001: a chrome sphere's
+   reflection then re-hits the sphere from inside and stays trapped until max_depth. */
+static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, float tmax, int origin) {
   f3 C = F3(s[0] + time * s[4], s[1] + time * s[5], s[2] + time * s[6]);
   f3 oc = fv_sub(o, C);
   float a = fdot(d, d);
@@ -852,6 +858,7 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   if (q == 0.0f || a == 0.0f) return -1.0f;
   float t0 = q / a, t1 = c / q;
   float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
+  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
   if (tmin < lo && lo < tmax) return lo;
   if (tmin < hi && hi < tmax) return hi;
   return -1.0f;
@@ -874,13 +881,15 @@ static float quad_t32(const float* q, f3 o, f3 d, float tmin, float tmax) {
 }
 
 /* closest hit: reference BVH order; boxes tested in f64 (pure culling), primitives in fp32 */
+/* `origin`: the primitive the ray starts on (-1 for camera rays). A quad is planar, so a ray
+   leaving it can never hit it again: it is skipped (DESIGN.md §4 "origin rule"). */
 static void node_hit32(const world32* w, int32_t code, f3 o, f3 d, const double O[3],
-                       const double Dd[3], float time, float* tbest, int64_t* best) {
+                       const double Dd[3], float time, int64_t origin, float* tbest, int64_t* best) {
   if (code < 0) {
     int64_t id = -1 - (int64_t)code;
     float t = w->s->prims[id].kind == RTG_PRIM_SPHERE
-                  ? sphere_t32(w->sph + id * 8, o, d, time, 0.001f, *tbest)
-                  : quad_t32(w->qd + id * 16, o, d, 0.001f, *tbest);
+                  ? sphere_t32(w->sph + id * 8, o, d, time, 0.001f, *tbest, id == origin)
+                  : (id == origin ? -1.0f : quad_t32(w->qd + id * 16, o, d, 0.001f, *tbest));
     if (t > 0.0f) {
       *tbest = t;
       *best = id;
@@ -889,8 +898,8 @@ static void node_hit32(const world32* w, int32_t code, f3 o, f3 d, const double 
   }
   const onode* n = &w->bvh.nodes[code];
   if (!box_hit(&n->box, O, Dd, 0.0009, (double)*tbest * (1 + 1e-6) + 1e-6)) return;
-  node_hit32(w, n->left, o, d, O, Dd, time, tbest, best);
-  if (n->right != n->left) node_hit32(w, n->right, o, d, O, Dd, time, tbest, best);
+  node_hit32(w, n->left, o, d, O, Dd, time, origin, tbest, best);
+  if (n->right != n->left) node_hit32(w, n->right, o, d, O, Dd, time, origin, tbest, best);
 }
 
 static float perlin_noise32(const float* vec, const rtg_perlin* pl, f3 p) {
@@ -980,13 +989,14 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
   float time = U(&st);
   f3 T = F3(1.0f, 1.0f, 1.0f), L = F3(0.0f, 0.0f, 0.0f);
   f3 bg = F3(cf[18], cf[19], cf[20]);
+  int64_t origin = -1; /* the primitive the current segment starts on */
   for (int depth = cam->max_depth; depth > 0; --depth) {
     float tbest = INFINITY;
     int64_t best = -1;
     (*segs)++;
     if (w->bvh.n > 0) {
       const double O[3] = {o.x, o.y, o.z}, Dd[3] = {d.x, d.y, d.z};
-      node_hit32(w, 0, o, d, O, Dd, time, &tbest, &best);
+      node_hit32(w, 0, o, d, O, Dd, time, origin, &tbest, &best);
     }
     if (best < 0) {
       L = fv_add(L, fmul3(T, bg));
@@ -1063,6 +1073,7 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
     T = fmul3(T, att);
     o = p;
     d = dir;
+    origin = best;
   }
   return L;
 }
@@ -1169,7 +1180,7 @@ int orc_kat_sphere_hit(const rtg_primitive* p, const double o[3], const double d
 /* the rtg-f32 sphere test (sphere_t32) on one record {center, r, motion, material}: t or -1 */
 float orc_sphere_t32(const float s[8], const float o[3], const float d[3], float time, float tmin,
                      float tmax) {
-  return sphere_t32(s, F3(o[0], o[1], o[2]), F3(d[0], d[1], d[2]), time, tmin, tmax);
+  return sphere_t32(s, F3(o[0], o[1], o[2]), F3(d[0], d[1], d[2]), time, tmin, tmax, 0);
 }
 int orc_kat_quad_hit(const rtg_primitive* p, const double o[3], const double d[3], double tmin,
                      double tmax, double rec[10], double bbox[6]) {

@@ -16,7 +16,9 @@
 // Modes:
 //   ref_harness golden                     -> JSON golden vectors on stdout
 //   ref_harness render SCENE W H SPP DEPTH SEED OUT.bin   -> fp64 framebuffer + segment count
-//   ref_harness bench SCENE W H SPP DEPTH PROCS           -> multi-process timing (JSON)
+//   ref_harness bench SCENE W H SPP DEPTH PROCS [ROWSTEP] -> multi-process timing (JSON)
+//   ref_harness moments SCENE W H SPP DEPTH PROCS SEED0 OUT.bin -> per-pixel sum L, sum L^2 (G5)
+//   ref_harness records GRID OUT.bin                      -> bouncing_spheres records (G1')
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -216,6 +218,23 @@ struct cam_t {
     color s = att * ray_color(scattered, depth - 1, world);
     return e + s;
   }
+  // Per-pixel first and second moments of one sample's radiance over every pixel of the image:
+  // out[(j*W + i)*6 + c] += L_c, out[... + 3 + c] += L_c^2, for samples_per_pixel samples of
+  // camera::render's loop order (camera.hpp:40-62). The statistical golden (G5) of the GPU.
+  void render_moments(const hittable& world, double* out) {
+    initialize();
+    for (int j = 0; j < image_height; ++j)
+      for (int i = 0; i < image_width; ++i) {
+        double* q = out + ((long)j * image_width + i) * 6;
+        for (int s = 0; s < samples_per_pixel; s++) {
+          const color L = ray_color(get_ray(i, j), max_depth, world);
+          for (int c = 0; c < 3; ++c) {
+            q[c] += L[c];
+            q[3 + c] += L[c] * L[c];
+          }
+        }
+      }
+  }
   // rows [r0, r0+nr): out = pixel_samples_scale * pixel_color (the input of write_color)
   void render(const hittable& world, int r0, int nr, double* out) {
     initialize();
@@ -312,9 +331,14 @@ static void setup_cam(const std::string& scene, cam_t& c) {
   c.lookfrom = point3(13.0f, 2.0f, 3.0f);
   c.defocus_angle = 0.0f;
   c.focus_dist = 10.0f;
-  if (scene == "book1") {
+  if (scene == "book1" || scene == "book1_g500") {
     c.defocus_angle = 0.6f;
   } else if (scene == "cornell") {  // main.cpp:325-342
+    c.background = color(0.0f, 0.0f, 0.0f);
+    c.vfov = 40.0f;
+    c.lookfrom = point3(278.0f, 278.0f, -800.0f);
+    c.lookat = point3(278.0f, 278.0f, 0.0f);
+  } else if (scene == "cornell_translate") {  // the Cornell camera
     c.background = color(0.0f, 0.0f, 0.0f);
     c.vfov = 40.0f;
     c.lookfrom = point3(278.0f, 278.0f, -800.0f);
@@ -327,12 +351,12 @@ static void setup_cam(const std::string& scene, cam_t& c) {
 }
 
 static std::shared_ptr<hittable> make_world(const std::string& scene) {
-  if (scene == "book1") {
-    hittable_list w = book1_world(11, false);
+  if (scene == "book1" || scene == "book1_g500") {  // g500: BASELINE config 5's 1M-sphere field
+    hittable_list w = book1_world(scene == "book1" ? 11 : 500, false);
     return std::make_shared<hittable_list>(std::make_shared<bvh_node>(w));  // main.cpp:76
   }
   auto w = std::make_shared<hittable_list>();
-  if (scene == "cornell") {  // main.cpp:301-322
+  if (scene == "cornell" || scene == "cornell_translate") {  // main.cpp:301-322
     auto red = std::make_shared<lambertian>(color(0.65f, 0.05f, 0.05f));
     auto white = std::make_shared<lambertian>(color(0.73f, 0.73f, 0.73f));
     auto green = std::make_shared<lambertian>(color(0.12f, 0.45f, 0.15f));
@@ -343,8 +367,20 @@ static std::shared_ptr<hittable> make_world(const std::string& scene) {
     w->add(std::make_shared<quad>(point3(0.0f, 0.0f, 0.0f), vec3(555.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, 555.0f), white));
     w->add(std::make_shared<quad>(point3(555.0f, 555.0f, 555.0f), vec3(-555.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, -555.0f), white));
     w->add(std::make_shared<quad>(point3(0.0f, 0.0f, 555.0f), vec3(555.0f, 0.0f, 0.0f), vec3(0.0f, 555.0f, 0.0f), white));
-    w->add(box(point3(130.0f, 0.0f, 65.0f), point3(295.0f, 165.0f, 230.0f), white));
-    w->add(box(point3(265.0f, 0.0f, 295.0f), point3(430.0f, 330.0f, 460.0f), white));
+    if (scene == "cornell") {
+      w->add(box(point3(130.0f, 0.0f, 65.0f), point3(295.0f, 165.0f, 230.0f), white));
+      w->add(box(point3(265.0f, 0.0f, 295.0f), point3(430.0f, 330.0f, 460.0f), white));
+    } else {  // the reference's own translate class (hittable.hpp:74-117), nested once
+      auto chrome = std::make_shared<metal>(color(0.8f, 0.85f, 0.88f), 0.0f);
+      w->add(std::make_shared<translate>(box(point3(0.0f, 0.0f, 0.0f), point3(165.0f, 330.0f, 165.0f), white),
+                                         vec3(265.0f, 0.0f, 295.0f)));
+      w->add(std::make_shared<translate>(
+          std::make_shared<translate>(box(point3(0.0f, 0.0f, 0.0f), point3(165.0f, 165.0f, 165.0f), white),
+                                      vec3(100.0f, 0.0f, 0.0f)),
+          vec3(30.0f, 0.0f, 65.0f)));
+      w->add(std::make_shared<translate>(std::make_shared<sphere>(point3(0.0f, 0.0f, 0.0f), 60.0f, chrome),
+                                         vec3(420.0f, 90.0f, 120.0f)));
+    }
   } else if (scene == "simple_light" || scene == "perlin") {  // main.cpp:174-207, 254-298
     auto pertext = std::make_shared<noise_texture>(4);
     w->add(std::make_shared<sphere>(point3(0.0f, -1000.0f, 0.0f), 1000.0f, std::make_shared<lambertian>(pertext)));
@@ -666,8 +702,10 @@ static int render_mode(const std::string& scene, int W, int H, int spp, int dept
   return 0;
 }
 
-// N processes, each renders every N-th row of the image with its own seed.
-static int bench_mode(const std::string& scene, int W, int H, int spp, int depth, int procs) {
+// N processes, each renders every N-th row of the image with its own seed. ROWSTEP > 1 renders
+// only rows 0, ROWSTEP, 2*ROWSTEP, ... (a bounded sample of the frame spread over its height).
+static int bench_mode(const std::string& scene, int W, int H, int spp, int depth, int procs, int rowstep) {
+  if (rowstep < 1) rowstep = 1;
   srand(1);
   std::shared_ptr<hittable> world = make_world(scene);
   std::vector<int> fds(procs);
@@ -688,7 +726,7 @@ static int bench_mode(const std::string& scene, int W, int H, int spp, int depth
       c.initialize();
       srand(1000 + k);
       std::vector<double> row(static_cast<size_t>(W) * 3);
-      for (int j = k; j < c.image_height; j += procs) c.render(*world, j, 1, row.data());
+      for (int j = k * rowstep; j < c.image_height; j += procs * rowstep) c.render(*world, j, 1, row.data());
       unsigned long long s = c.segments;
       if (write(p[1], &s, sizeof(s)) != (ssize_t)sizeof(s)) _exit(1);
       _exit(0);
@@ -711,15 +749,96 @@ static int bench_mode(const std::string& scene, int W, int H, int spp, int depth
   return 0;
 }
 
+// G5: PROCS processes each render the whole image at SPP samples per pixel from their own
+// srand(SEED0 + k) stream and return per-pixel moments (sum L, sum L^2, per channel); the parent
+// writes their sum, (H, W, 6) doubles, to OUT. Every pixel then carries PROCS*SPP independent
+// samples of the reference's estimator.
+static int moments_mode(const std::string& scene, int W, int H, int spp, int depth, int procs,
+                        unsigned seed0, const char* outpath) {
+  srand(1);
+  std::shared_ptr<hittable> world = make_world(scene);
+  cam_t c0;
+  setup_cam(scene, c0);
+  c0.image_width = W;
+  c0.aspect_ratio = static_cast<double>(W) / H;
+  c0.samples_per_pixel = spp;
+  c0.max_depth = depth;
+  c0.initialize();
+  const size_t n = static_cast<size_t>(c0.image_width) * c0.image_height * 6;
+  const std::string base(outpath);
+  std::vector<pid_t> pids(procs);
+  for (int k = 0; k < procs; ++k) {
+    pid_t pid = fork();
+    if (pid == 0) {
+      cam_t c = c0;
+      srand(seed0 + k);
+      std::vector<double> m(n, 0.0);
+      c.render_moments(*world, m.data());
+      FILE* f = fopen((base + ".part" + std::to_string(k)).c_str(), "wb");
+      if (!f || fwrite(m.data(), sizeof(double), n, f) != n) _exit(1);
+      fclose(f);
+      printf("%llu\n", c.segments);
+      fflush(stdout);
+      _exit(0);
+    }
+    pids[k] = pid;
+  }
+  std::vector<double> sum(n, 0.0), part(n);
+  for (int k = 0; k < procs; ++k) {
+    int status = 0;
+    waitpid(pids[k], &status, 0);
+    if (!WIFEXITED(status) || WEXITSTATUS(status) != 0) return 1;
+    const std::string p = base + ".part" + std::to_string(k);
+    FILE* f = fopen(p.c_str(), "rb");
+    if (!f || fread(part.data(), sizeof(double), n, f) != n) return 1;
+    fclose(f);
+    remove(p.c_str());
+    for (size_t i = 0; i < n; ++i) sum[i] += part[i];
+  }
+  FILE* f = fopen(outpath, "wb");
+  if (!f) return 1;
+  fwrite(sum.data(), sizeof(double), n, f);
+  fclose(f);
+  printf("{\"width\": %d, \"height\": %d, \"samples_per_pixel\": %d}\n", c0.image_width, c0.image_height,
+         spp * procs);
+  return 0;
+}
+
+// G1': the bouncing_spheres records of grid half-width GRID (main.cpp:12-76 with the loop bounds
+// generalised), from the default seed-1 stream, as (N, 13) doubles: c1[3] c2[3] r mat albedo[3]
+// fuzz ri (mat: 0 ground checker, 1 lambertian, 2 metal, 3 dielectric).
+static int records_mode(int grid, const char* outpath) {
+  srand(1);
+  g_book1.clear();
+  book1_world(grid, true);
+  FILE* f = fopen(outpath, "wb");
+  if (!f) return 1;
+  long counts[4] = {0, 0, 0, 0};
+  for (const sphere_rec& s : g_book1) {
+    const double row[13] = {s.c1[0], s.c1[1], s.c1[2], s.c2[0], s.c2[1], s.c2[2], s.r, double(s.mat),
+                            s.albedo[0], s.albedo[1], s.albedo[2], s.fuzz, s.ri};
+    fwrite(row, sizeof(double), 13, f);
+    counts[s.mat]++;
+  }
+  fclose(f);
+  printf("{\"records\": %zu, \"ground\": %ld, \"lambertian\": %ld, \"metal\": %ld, \"dielectric\": %ld}\n",
+         g_book1.size(), counts[0], counts[1], counts[2], counts[3]);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && std::string(argv[1]) == "golden") return golden();
+  if (argc >= 10 && std::string(argv[1]) == "moments")
+    return moments_mode(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]),
+                        (unsigned)strtoul(argv[8], nullptr, 10), argv[9]);
+  if (argc >= 4 && std::string(argv[1]) == "records") return records_mode(atoi(argv[2]), argv[3]);
   if (argc >= 9 && std::string(argv[1]) == "render")
     return render_mode(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
                        (unsigned)strtoul(argv[7], nullptr, 10), argv[8]);
   if (argc >= 8 && std::string(argv[1]) == "bench")
     return bench_mode(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
-                      atoi(argv[7]));
+                      atoi(argv[7]), argc >= 9 ? atoi(argv[8]) : 1);
   fprintf(stderr,
-          "usage: ref_harness golden | render SCENE W H SPP DEPTH SEED OUT | bench SCENE W H SPP DEPTH PROCS\n");
+          "usage: ref_harness golden | render SCENE W H SPP DEPTH SEED OUT | bench SCENE W H SPP DEPTH PROCS [ROWSTEP]\n");
   return 2;
 }

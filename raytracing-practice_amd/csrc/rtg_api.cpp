@@ -61,6 +61,20 @@ rtg_status hip_fail(hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(e_, what); \
   } while (0)
 
+// Stream-ordered scratch of one render (stack spill, wave trace, chunk partial sums): freed on
+// the render stream on every exit, the early error returns included, so a failed launch never
+// leaks the (config 5: 6.3 GB) partial-sum buffer.
+struct StreamScratch {
+  hipStream_t stream = nullptr;
+  void* ptr[4] = {};
+  int n = 0;
+  void** add() { return &ptr[n++]; }
+  ~StreamScratch() {
+    for (int k = 0; k < n; ++k)
+      if (ptr[k]) (void)hipFreeAsync(ptr[k], stream);  // teardown: nothing to report to
+  }
+};
+
 // ---- fp64 vector helpers with the reference's operator semantics (vec3.hpp:100-155) ----
 struct D3 {
   double x, y, z;
@@ -702,6 +716,11 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     hs.num_nodes = r.num_nodes;
     hs.depth = r.depth;
     hs.stack_need = r.stack_need;
+    // the device tree's bound is only known now; the 4-wide LDS node step has no overflow check
+    // outside the COUNT diagnostics, so this host-side bound is the guard (as for host builds)
+    if (hs.stack_need > kMaxStackNeed)
+      return cleanup(fail(RTG_E_UNSUPPORTED, "device BVH needs " + std::to_string(hs.stack_need) +
+                                                 " stack entries (limit " + std::to_string(kMaxStackNeed) + ")"));
     gpu_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t2).count();
   }
 
@@ -939,10 +958,13 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     dj.lds_stack = std::min(stack_depth, std::max(1, std::atoi(e)));
   dj.spill_depth = (variant == 3 || variant == 0) ? std::max(0, need - dj.lds_stack) : 0;
   dj.spill = nullptr;
+  StreamScratch scratch;
+  scratch.stream = stream;
   if (dj.spill_depth > 0)
-    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.spill),
+    RTG_HIP(hipMallocAsync(scratch.add(),
                            static_cast<size_t>(grid_waves) * 64 * dj.spill_depth * sizeof(int32_t), stream),
             "hipMallocAsync(stack spill)");
+  if (dj.spill_depth > 0) dj.spill = static_cast<int32_t*>(scratch.ptr[scratch.n - 1]);
   dj.counters = s->counters;
   RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
   // optional per-wave timeline for schedule analysis (tools/wave_trace.py)
@@ -951,15 +973,17 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (trace_path) {
     trace_slots = variant == 3 || variant == 0 ? int64_t(grid_waves)
                                                : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
-    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.trace), trace_slots * 32, stream), "hipMalloc(trace)");
+    RTG_HIP(hipMallocAsync(scratch.add(), trace_slots * 32, stream), "hipMalloc(trace)");
+    dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
   }
   if (progressive && !(variant == 3 || variant == 0))
     return fail(RTG_E_INVALID, "progressive rendering needs the default schedules");
   const bool chunked = !progressive && dj.chunks > 1 && (variant == 3 || variant == 0) && dc.max_depth > 0;
-  if (chunked)
-    RTG_HIP(hipMallocAsync(reinterpret_cast<void**>(&dj.partial), out_bytes * dj.chunks, stream),
-            "hipMallocAsync(partial sums)");
+  if (chunked) {
+    RTG_HIP(hipMallocAsync(scratch.add(), out_bytes * dj.chunks, stream), "hipMallocAsync(partial sums)");
+    dj.partial = static_cast<float*>(scratch.ptr[scratch.n - 1]);
+  }
   if (!(variant == 3 || variant == 0)) {  // schedules 1 and 2 keep one running sum per pixel
     dj.chunks = 1;
     dj.chunk_samples = std::max(1, cam->samples_per_pixel);
@@ -978,13 +1002,10 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, sum_chunks, out_scale, stream),
             "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
-  if (chunked) RTG_HIP(hipFreeAsync(dj.partial, stream), "hipFreeAsync(partial sums)");
-  if (dj.spill) RTG_HIP(hipFreeAsync(dj.spill, stream), "hipFreeAsync(stack spill)");
   if (trace_path) {
     std::vector<unsigned long long> tr(static_cast<size_t>(trace_slots) * 4);
     RTG_HIP(hipMemcpyAsync(tr.data(), dj.trace, trace_slots * 32, hipMemcpyDeviceToHost, stream), "trace copy");
     RTG_HIP(hipStreamSynchronize(stream), "trace sync");
-    RTG_HIP(hipFree(dj.trace), "trace free");
     if (FILE* f = std::fopen(trace_path, "wb")) {
       std::fwrite(tr.data(), 8, tr.size(), f);
       std::fclose(f);

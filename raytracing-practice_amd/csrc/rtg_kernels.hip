@@ -109,9 +109,12 @@ __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
 // is formed in f64 for spheres of radius >= kSphereF64Radius (a ground sphere, where fp32
 // cancellation would put self-hits above tmin), in fp32 below it, where the discriminant is
 // taken from the centre-to-line distance; the near root is c/q. Returns the root or -1.
+// `origin`: the ray starts on this sphere (its previous segment hit it): only the far root of a
+// ray entering the sphere counts (DESIGN.md §4 "origin rule"; fp32 puts the origin ~ulp(|p|) off
+// the surface, and a grazing ray's own root could pass tmin and trap a reflection inside).
 constexpr float kSphereF64Radius = 16.0f;
 __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float time, float tmin,
-                                          float tmax) {
+                                          float tmax, bool origin) {
   const V3 C = v3(s0.x + time * s1.x, s0.y + time * s1.y, s0.z + time * s1.z);
   const V3 oc = sub(o, C);
   const float a = dot(d, d);
@@ -142,6 +145,7 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float t1 = c / q;
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
+  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
   if (tmin < lo && lo < tmax) return lo;
   if (tmin < hi && hi < tmax) return hi;
   return -1.0f;
@@ -183,10 +187,11 @@ struct Trav {
   int32_t best;   // primitive ref of the closest hit, -1 = none
   int32_t todo;   // inner node (>= 0: index, or byte offset in 4-wide trees) or leaf code (< 0)
   int32_t sp;     // stack depth
+  int32_t origin; // primitive ref the ray starts on (-1: camera ray), DESIGN.md §4 "origin rule"
   bool active;    // traversal not finished
 };
 
-__device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d) {
+__device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d, int32_t origin) {
   t.ix = __builtin_amdgcn_rcpf(d.x);
   t.iy = __builtin_amdgcn_rcpf(d.y);
   t.iz = __builtin_amdgcn_rcpf(d.z);
@@ -200,6 +205,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.best = -1;
   t.todo = S.root_code;
   t.sp = 0;
+  t.origin = origin;
   t.active = S.num_nodes > 0;
 }
 
@@ -437,7 +443,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * 2;
       if (COUNT) cnt.prim += 1;
-      const float th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest);
+      const float th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest, first + k == t.origin);
       if (th > 0.0f) {
         t.tbest = th;
         t.best = first + k;
@@ -450,11 +456,12 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     const int32_t ref = S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit);
     float th;
     if (COUNT) cnt.prim += 1;
-    if (ref & kQuadRefBit) {
-      th = quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, t.tbest);
+    if (ref & kQuadRefBit) {  // planar: a ray leaving a quad never hits it again
+      th = ref == t.origin ? -1.0f
+                           : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, t.tbest);
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
-      th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest);
+      th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest, ref == t.origin);
     }
     if (th > 0.0f) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
@@ -480,7 +487,7 @@ __device__ __forceinline__ void trav_step(Trav& t, const DevScene& S, V3 o, V3 d
 // aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
 // traversal: the nearer child first, the farther pushed on the lane's LDS stack.
 template <int STACK, bool COUNT>
-__device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, float time,
+__device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, float time, int32_t origin,
                                                float& tbest, int32_t* stk, Counts<COUNT>& cnt,
                                                bool& overflow, bool& corrupt) {
   int32_t best = -1;
@@ -546,10 +553,11 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
         float t;
         if (COUNT) cnt.prim += 1;
         if (ref & kQuadRefBit) {
-          t = quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest);
+          t = ref == origin ? -1.0f
+                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest);
         } else {
           const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
-          t = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, tbest);
+          t = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, tbest, ref == origin);
         }
         if (t > 0.0f) {  // t > tmin >= 0.001 on a hit
           tbest = t;
@@ -659,6 +667,7 @@ struct PathState {
   float time;
   V3 T, L;
   int depth;
+  int32_t origin;  // primitive ref the current segment starts on (-1: camera ray)
   uint64_t rng;
 };
 
@@ -690,6 +699,7 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
   ps.T = v3(1.0f, 1.0f, 1.0f);
   ps.L = v3(0.0f, 0.0f, 0.0f);
   ps.depth = C.max_depth;
+  ps.origin = -1;
 }
 
 // Shades the closest hit `ref` at distance t; returns false when the path ends
@@ -788,6 +798,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   ps.T = mul(ps.T, att);
   ps.o = p;
   ps.d = dir;
+  ps.origin = ref;
   return true;
 }
 
@@ -967,11 +978,11 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     }
     if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
     if (fresh || cont) {
-      trav_begin(tr, S, ps.o, ps.d);
+      trav_begin(tr, S, ps.o, ps.d, ps.origin);
       if (S.occluder >= 0) {  // the scene-spanning sphere kept out of the BVH (DevScene::occluder)
         const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * 2;
         if (COUNT) w.cnt.prim += 1;
-        const float th = sphere_t(sp4[0], sp4[1], ps.o, ps.d, ps.time, kTMin, tr.tbest);
+        const float th = sphere_t(sp4[0], sp4[1], ps.o, ps.d, ps.time, kTMin, tr.tbest, S.occluder == ps.origin);
         if (th > 0.0f) {
           tr.tbest = th;
           tr.best = S.occluder;
@@ -1187,7 +1198,7 @@ __global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCame
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   while (sample < C.spp) {
     Trav tr;
-    trav_begin(tr, S, ps.o, ps.d);
+    trav_begin(tr, S, ps.o, ps.d, ps.origin);
     while (tr.active)
       trav_step<LdsStack<STACK>, COUNT>(tr, S, ps.o, ps.d, ps.time, LdsStack<STACK>{stk}, cnt, overflow, corrupt);
     ++segs;
@@ -1241,7 +1252,7 @@ __global__ __launch_bounds__(256) void render_kernel_v0(DevScene S, DevCamera C,
   while (sample < C.spp) {
     float t = __builtin_inff();
     const int32_t ref =
-        closest_hit<STACK, COUNT>(S, ps.o, ps.d, ps.time, t, stk, cnt, overflow, corrupt);
+        closest_hit<STACK, COUNT>(S, ps.o, ps.d, ps.time, ps.origin, t, stk, cnt, overflow, corrupt);
     ++segs;
     bool alive;
     if (ref < 0) {
@@ -1280,15 +1291,19 @@ __global__ __launch_bounds__(256) void render_kernel_v0(DevScene S, DevCamera C,
   if (__any(corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
 }
 
-// write_color (color.hpp:14-58): sqrt gamma, clamp to [0, 0.999], int(256 * x).
+// write_color (color.hpp:14-58) in the reference's own precision: linear_to_gamma takes the
+// square root in double (color.hpp:14-23), interval::clamp clamps in double to
+// [0.000f, 0.999f] (the float literals widened, color.hpp:45, interval.hpp:35-46), and
+// int(256 * x) truncates the double product — so every byte equals the reference's.
 __global__ __launch_bounds__(256) void resolve_kernel(const float* __restrict__ in,
                                                       uint8_t* __restrict__ out, int64_t n) {
   const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (k >= n * 3) return;
-  float x = in[k];
-  x = x > 0.0f ? sqrtf(x) : 0.0f;
-  x = x < 0.0f ? 0.0f : (x > 0.999f ? 0.999f : x);
-  out[k] = static_cast<uint8_t>(static_cast<int>(256.0f * x));
+  double x = static_cast<double>(in[k]);
+  x = x > 0.0 ? __builtin_sqrt(x) : 0.0;  // llvm.sqrt.f64: correctly rounded on gfx950
+  const double lo = static_cast<double>(0.000f), hi = static_cast<double>(0.999f);
+  x = x < lo ? lo : (x > hi ? hi : x);
+  out[k] = static_cast<uint8_t>(static_cast<int>(256.0 * x));
 }
 
 // Pixel = scale * (((p_0 + p_1) + p_2) + ...): the chunk partial sums in chunk order.

@@ -178,6 +178,30 @@ inline scene cornell_box() {  // main.cpp:301-346
   return s;
 }
 
+// Regression scene for translate (hittable.hpp:74-117; not in main.cpp): the Cornell box with its
+// two boxes built at the origin and moved by translate (one of them by a translate of a translate)
+// plus a translated metal sphere, so quads, spheres and nested offsets all go through
+// translate::rtg_flatten. oracle/ref_harness.cpp builds the same scene with the reference's own
+// translate class for the statistical golden.
+inline scene cornell_translate() {
+  scene s = cornell_box();
+  auto world = std::make_shared<hittable_list>();
+  auto& objs = std::static_pointer_cast<hittable_list>(s.world)->objects;
+  for (size_t k = 0; k < 6; ++k) world->add(objs[k]);  // the five walls and the light
+  auto white = std::make_shared<lambertian>(color(0.73f, 0.73f, 0.73f));
+  auto chrome = std::make_shared<metal>(color(0.8f, 0.85f, 0.88f), 0.0f);
+  world->add(std::make_shared<translate>(box(point3(0.0f, 0.0f, 0.0f), point3(165.0f, 330.0f, 165.0f), white),
+                                         vec3(265.0f, 0.0f, 295.0f)));
+  world->add(std::make_shared<translate>(
+      std::make_shared<translate>(box(point3(0.0f, 0.0f, 0.0f), point3(165.0f, 165.0f, 165.0f), white),
+                                  vec3(100.0f, 0.0f, 0.0f)),
+      vec3(30.0f, 0.0f, 65.0f)));
+  world->add(std::make_shared<translate>(std::make_shared<sphere>(point3(0.0f, 0.0f, 0.0f), 60.0f, chrome),
+                                         vec3(420.0f, 90.0f, 120.0f)));
+  s.world = world;
+  return s;
+}
+
 // Benchmark config 3: Perlin ground of perlin_sphere + the earth globe, drawn in
 // that order so the Perlin tables come first from the seed-1 stream.
 inline scene earth_perlin() {
@@ -204,6 +228,7 @@ inline const std::map<std::string, std::function<scene(int)>>& registry() {
       {"quads", [](int) { return quads(); }},
       {"simple_light", [](int) { return simple_light(); }},
       {"cornell_box", [](int) { return cornell_box(); }},
+      {"cornell_translate", [](int) { return cornell_translate(); }},
       {"earth_perlin", [](int) { return earth_perlin(); }},
   };
   return r;

@@ -24,7 +24,7 @@ class Oracle:
         L.orc_render_f64.argtypes = [P(rtgpu.rtg_scene_desc), P(rtgpu.rtg_camera_desc), C.c_uint,
                                      C.c_int, C.c_int, C.c_void_p, P(C.c_uint64)]
         L.orc_bench_f64.argtypes = [P(rtgpu.rtg_scene_desc), P(rtgpu.rtg_camera_desc), C.c_int,
-                                    C.c_int, C.c_uint, P(C.c_double), P(C.c_uint64)]
+                                    C.c_int, C.c_int, C.c_uint, P(C.c_double), P(C.c_uint64)]
         L.orc_glibc_random_double.argtypes = [C.c_uint, C.c_int]
         L.orc_glibc_random_double.restype = C.c_double
         L.orc_rng_state.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
@@ -90,9 +90,9 @@ class Oracle:
                                 out.ctypes.data, C.byref(segs))
         return out, segs.value
 
-    def bench_f64(self, desc, cam, threads, rows, base_seed=1000):
+    def bench_f64(self, desc, cam, threads, rows, base_seed=1000, row_step=1):
         sec, segs = C.c_double(0), C.c_uint64(0)
-        self.lib.orc_bench_f64(C.byref(desc), C.byref(cam), threads, rows, base_seed,
+        self.lib.orc_bench_f64(C.byref(desc), C.byref(cam), threads, rows, row_step, base_seed,
                                C.byref(sec), C.byref(segs))
         return sec.value, segs.value
 

@@ -28,7 +28,7 @@ def hybrid_camera(scene, W, H, spp, depth):
     kw["background"] = tuple(float(np.float32(x)) for x in kw["background"])
     if scene == "book1":
         kw["defocus_angle"] = float(np.float32(0.6))
-    elif scene == "cornell":
+    elif scene in ("cornell", "cornell_translate"):
         kw.update(background=(0, 0, 0), vfov=40.0, lookfrom=(278, 278, -800), lookat=(278, 278, 0))
     elif scene == "simple_light":
         kw.update(background=(0, 0, 0), lookfrom=(26, 3, 6), lookat=(0, 2, 0))

@@ -10,7 +10,7 @@ cur = None
 for line in sys.stdin:
     m = re.search(r"Function Name: (\S+)", line)
     if m:
-        cur = m.group(1); print(cur[:60], end=""); continue
+        cur = m.group(1); print(cur[:90], end=""); continue
     for key in ("VGPRs:", "SGPRs Spill:", "ScratchSize [bytes/lane]:", "Occupancy [waves/SIMD]:", "LDS Size [bytes/block]:"):
         if key in line:
             print("  %s %s" % (key.split()[0], line.split(key)[1].split()[0]), end="")

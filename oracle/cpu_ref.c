@@ -837,13 +837,13 @@ static void world32_free(world32* w) {
 static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, float tmax, int origin) {
   f3 C = F3(s[0] + time * s[4], s[1] + time * s[5], s[2] + time * s[6]);
   f3 oc = fv_sub(o, C);
-  float a = fdot(d, d);
+  float a = fdot(d, d), inv_a = 1.0f / a; /* per ray on the GPU (Trav::a, inv_a) */
   float hb = fdot(oc, d);
   float c, disc;
   if (fabsf(s[3]) < 16.0f) {
     /* disc = a (r^2 - |oc - (h/a) d|^2), 1/a rounded first */
     c = fdot(oc, oc) - s[3] * s[3];
-    float inv_a = 1.0f / a, sh = hb * inv_a;
+    float sh = hb * inv_a;
     f3 f = F3(oc.x - sh * d.x, oc.y - sh * d.y, oc.z - sh * d.z);
     disc = a * (s[3] * s[3] - fdot(f, f));
   } else {
@@ -856,7 +856,7 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   float sq = sqrtf(disc);
   float q = -(hb + copysignf(sq, hb));
   if (q == 0.0f || a == 0.0f) return -1.0f;
-  float t0 = q / a, t1 = c / q;
+  float t0 = q * inv_a, t1 = c / q; /* far root by the reciprocal, near root divided */
   float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
   if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
   if (tmin < lo && lo < tmax) return lo;

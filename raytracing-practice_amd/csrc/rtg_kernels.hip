@@ -113,11 +113,12 @@ __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
 // ray entering the sphere counts (DESIGN.md §4 "origin rule"; fp32 puts the origin ~ulp(|p|) off
 // the surface, and a grazing ray's own root could pass tmin and trap a reflection inside).
 constexpr float kSphereF64Radius = 16.0f;
-__device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float time, float tmin,
-                                          float tmax, bool origin) {
+// a = d.d and inv_a = 1/a (correctly rounded) are per ray (Trav): the far root is q * inv_a and
+// only the near root c / q is a division.
+__device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float a, float inv_a, float time,
+                                          float tmin, float tmax, bool origin) {
   const V3 C = v3(s0.x + time * s1.x, s0.y + time * s1.y, s0.z + time * s1.z);
   const V3 oc = sub(o, C);
-  const float a = dot(d, d);
   const float hb = dot(oc, d);
   float c, disc;
   if (fabsf(s0.w) < kSphereF64Radius) {
@@ -125,7 +126,6 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
     // disc = a (r^2 - |f|^2), f = oc - (h/a) d the centre-to-line offset: no h^2 - a c
     // cancellation, so a grazing ray far from a small sphere is classified to ~r^2 2^-22, not
     // ~h^2 2^-24 (a false hit outside the sphere's box, which box culling precision then decides)
-    const float inv_a = 1.0f / a;
     const float s = hb * inv_a;
     const V3 f = v3(oc.x - s * d.x, oc.y - s * d.y, oc.z - s * d.z);
     disc = a * (s0.w * s0.w - dot(f, f));
@@ -141,7 +141,7 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float sq = sqrtf(disc);
   const float q = -(hb + copysignf(sq, hb));
   if (q == 0.0f || a == 0.0f) return -1.0f;
-  const float t0 = q / a;
+  const float t0 = q * inv_a;
   const float t1 = c / q;
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
@@ -180,7 +180,8 @@ struct Counts {
 // -> aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
 // traversal: the nearer child first, the farther one pushed on the lane's LDS stack.
 struct Trav {
-  float ix, iy, iz;  // 1/d
+  float ix, iy, iz;  // 1/d (approximate: culling only)
+  float a, inv_a;    // d.d and its correctly rounded reciprocal (sphere_t)
   float ox, oy, oz;  // -o/d, for the fused slab test
   int32_t sx, sy, sz;  // 4-wide nodes: byte offset (0 or 48) of each axis' near-plane row
   float tbest;    // closest hit so far (the shrinking interval.max of the reference)
@@ -198,6 +199,8 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.sx = (static_cast<uint32_t>(ibits(t.ix)) >> 31) * 48;
   t.sy = (static_cast<uint32_t>(ibits(t.iy)) >> 31) * 48;
   t.sz = (static_cast<uint32_t>(ibits(t.iz)) >> 31) * 48;
+  t.a = dot(d, d);
+  t.inv_a = 1.0f / t.a;
   t.ox = -o.x * t.ix;
   t.oy = -o.y * t.iy;
   t.oz = -o.z * t.iz;
@@ -443,7 +446,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * 2;
       if (COUNT) cnt.prim += 1;
-      const float th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest, first + k == t.origin);
+      const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
       if (th > 0.0f) {
         t.tbest = th;
         t.best = first + k;
@@ -461,7 +464,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, t.tbest);
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
-      th = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, t.tbest, ref == t.origin);
+      th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
     }
     if (th > 0.0f) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
@@ -495,6 +498,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
   const V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y),
                     __builtin_amdgcn_rcpf(d.z));
   const V3 oi = v3(-o.x * inv.x, -o.y * inv.y, -o.z * inv.z);
+  const float a = dot(d, d), inv_a = 1.0f / a;
   int sp = 0;
   int32_t todo = 0;
   while (true) {
@@ -557,7 +561,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
                             : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest);
         } else {
           const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
-          t = sphere_t(sp4[0], sp4[1], o, d, time, kTMin, tbest, ref == origin);
+          t = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
         }
         if (t > 0.0f) {  // t > tmin >= 0.001 on a hit
           tbest = t;
@@ -617,6 +621,9 @@ __device__ float perlin_turb(const float4* vec, const int32_t* perm, V3 p) {
 // the perlin and image paths cost ~12 vector registers the common scenes would otherwise spill.
 template <bool FULL>
 __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3 p) {
+  // a checker resolves to another texture: one trip per nesting level (solid under checker: 2);
+  // not unrolled (16 unrolled copies cost ~70 scalar branch instructions per shade)
+#pragma unroll 1
   for (int guard = 0; guard < kMaxTexNesting; ++guard) {
     const float4 t0 = S.textures[tex * 2];
     const float4 t1 = S.textures[tex * 2 + 1];
@@ -982,7 +989,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       if (S.occluder >= 0) {  // the scene-spanning sphere kept out of the BVH (DevScene::occluder)
         const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * 2;
         if (COUNT) w.cnt.prim += 1;
-        const float th = sphere_t(sp4[0], sp4[1], ps.o, ps.d, ps.time, kTMin, tr.tbest, S.occluder == ps.origin);
+        const float th = sphere_t(sp4[0], sp4[1], ps.o, ps.d, tr.a, tr.inv_a, ps.time, kTMin, tr.tbest,
+                                  S.occluder == ps.origin);
         if (th > 0.0f) {
           tr.tbest = th;
           tr.best = S.occluder;

@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--gather", choices=["f32", "rgb8"], default="f32",
                     help="gather the linear fp32 frame (default) or the write_color bytes (4x fewer)")
+    ap.add_argument("--gather-impl", choices=["rtg", "torch"], default="rtg",
+                    help="N>1: the C-ABI's RCCL gather + de-interleave kernel (rtg_gather_rows, default) or "
+                         "torch.distributed.gather + a torch de-interleave")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="wall time the all-cores CPU sample is sized for (the 1-core sample adds ~3-5 s)")
@@ -164,6 +167,20 @@ def pmc_traffic(workload):
     return None
 
 
+def pmc_binding(workload):
+    """The binding resource of the render kernel for this workload (profiles/pmc_binding.json, written
+    by tools/pmc_report.py --write-binding from rocprofv3 PMC passes of the same command): VALU issue
+    fraction, lane utilisation, wave-cycle split, LDS bank conflicts. None when not measured."""
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_binding.json")) as f:
+            rec = json.load(f)
+        if rec.get("workload") == workload:
+            return rec
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -198,6 +215,15 @@ def main():
     shard = torch.zeros((rtgpu.padded_rows(H, world), W, 3), dtype=torch.float32, device="cuda")
     shard8 = torch.zeros(shard.shape, dtype=torch.uint8, device="cuda") if args.gather == "rgb8" else None
     stream = torch.cuda.current_stream().cuda_stream
+    comm, frame = None, None
+    if world > 1 and args.gather_impl == "rtg":
+        # one RCCL communicator of the C-ABI (rtg_comm_create_rank), its id shared over torch.distributed
+        uid = [lib.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = lib.comm_rank(uid[0], world, rank, local)
+        if rank == 0:
+            frame = torch.zeros((H, W, 3), dtype=(torch.uint8 if shard8 is not None else torch.float32),
+                                device="cuda")
 
     def step(i):
         # a rank past the image's last row renders nothing (its shard stays zero padding)
@@ -206,7 +232,12 @@ def main():
         if shard8 is not None:  # write_color on the device (rtg_resolve_rgb8), gather the bytes
             ds.resolve_rgb8(shard.data_ptr(), shard8.data_ptr(), shard.shape[0] * W, stream)
         if world > 1:
-            rtgpu.gather_frame(shard8 if shard8 is not None else shard, H)
+            src = shard8 if shard8 is not None else shard
+            if comm is not None:  # ncclGather to rank 0 + the de-interleave kernel there (rtg_gather_rows)
+                comm.gather_rows([src.data_ptr()], H, W * 3 * src.element_size(), 0,
+                                 frame.data_ptr() if frame is not None else 0, [stream])
+            else:
+                rtgpu.gather_frame(src, H)
         return st
 
     for i in range(args.warmup):
@@ -262,8 +293,9 @@ def main():
             "config": {"workload": workload, "baseline_config": args.config, "scene": args.scene,
                        "grid": args.grid, "width": W,
                        "height": H, "spp": args.spp, "depth": args.depth, "bvh": args.bvh,
-                       "parallelism": (f"rows interleaved over {world} GPUs, one RCCL gather ({args.gather}) of the "
-                                       f"frame to rank 0 per step" if world > 1 else
+                       "parallelism": (f"rows interleaved over {world} GPUs, one RCCL gather ({args.gather}, "
+                                       f"{'rtg_gather_rows' if args.gather_impl == 'rtg' else 'torch.distributed'}) "
+                                       f"of the frame to rank 0 per step" if world > 1 else
                                        "1 GPU, whole frame (no gather)")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -273,6 +305,7 @@ def main():
                                   "or L2/MALL for scenes too large for LDS); traffic = PMC-measured HBM bytes "
                                   "per launch (null when not measured for this workload); the binding "
                                   "resource is VALU issue and LDS/cache latency (DESIGN.md section 6)"),
+                         "binding": pmc_binding(workload),
                          "kernel_ms": round(avg_kernel_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(algo_bytes),
                          "per_segment": {"box_tests": round(cst.box_tests / max(cst.segments, 1), 3),
@@ -292,6 +325,9 @@ def main():
             line["speedup_vs_cpu_one_core"] = (round(line["value"] / cb["one_core"]["value"], 1)
                                                if cb["one_core"]["value"] else None)
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     ds.close()
     if world > 1:
         dist.destroy_process_group()

@@ -154,9 +154,11 @@ typedef struct rtg_camera_params {
 #define RTG_RENDER_ASYNC 0x2      /* do not synchronize (requires OUT_DEVICE); stats filled later */
 #define RTG_RENDER_COUNT 0x4      /* also count box / primitive tests (slower, diagnostic) */
 /* Diagnostic schedule selection (A/B of kernel variants; 0 = the default everywhere):
- * bits 8-15 schedule (0 default = 3 when the scene geometry fits in LDS else 4; 1 one closest-hit
- * query per loop trip; 2 the first kernel (1 and 2 need a binary BVH: RTG_BVH_MEDIAN); 3
- * persistent 16-wave workgroups with LDS-resident geometry; 4 ballot-batched on a plain grid),
+ * bits 8-15 schedule (0 default = 3 when the scene geometry fits in LDS, else 5 for 4-wide trees,
+ * else 4; 1 one closest-hit query per loop trip; 2 the first kernel (1 and 2 need a binary BVH:
+ * RTG_BVH_MEDIAN); 3 persistent 16-wave workgroups with LDS-resident geometry; 4 ballot-batched on
+ * a plain grid, scene through the caches; 5 the persistent workgroups with the breadth-first top
+ * of a 4-wide tree in LDS and the rest through the caches),
  * bits 16-23 shade batch of schedule 0 in 64ths of the live lanes (0 = library default). */
 #define RTG_RENDER_SCHEDULE(n) (((n) & 0xff) << 8)
 #define RTG_RENDER_SHADE_BATCH(n) (((n) & 0xff) << 16)
@@ -258,6 +260,48 @@ rtg_status rtg_render_wait(rtg_scene* scene, rtg_render_stats* stats);
  * in_rgb / out_rgb8 are device pointers on the scene's device; n_pixels pixels. */
 rtg_status rtg_resolve_rgb8(rtg_scene* scene, const float* in_rgb, uint8_t* out_rgb8,
                             int64_t n_pixels, void* stream);
+
+/* ---- multi-GPU frames: row-interleaved shards, one RCCL gather over xGMI ----
+ * Replaces the reference's single-device pixel loop of camera::render (camera.hpp:29-72) when the
+ * image is tiled over several GPUs: rank r renders rows r, r+N, r+2N, ... (any N gives the same
+ * image: the RNG is keyed by the global pixel), every shard is padded to ceil(H/N) rows, and the
+ * root receives them with one ncclGather, then de-interleaves them on its device.
+ * A communicator spans N ranks; a process holds one of them (one process per GPU, ids shared out
+ * of band) or all of them (one process driving every local GPU, ncclCommInitAll). */
+typedef struct rtg_comm rtg_comm;
+#define RTG_COMM_ID_BYTES 128
+
+/* One process, `ndev` local devices: ranks 0..ndev-1 are devices[0..ndev-1]. */
+rtg_status rtg_comm_create_local(const int32_t* devices, int32_t ndev, rtg_comm** out);
+/* One process per device: rank 0 calls rtg_comm_unique_id and hands the bytes to every rank. */
+rtg_status rtg_comm_unique_id(uint8_t id[RTG_COMM_ID_BYTES]);
+rtg_status rtg_comm_create_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank,
+                                int32_t device, rtg_comm** out);
+/* nranks: ranks of the communicator; nlocal: ranks this process drives. */
+rtg_status rtg_comm_size(const rtg_comm* comm, int32_t* nranks, int32_t* nlocal);
+void rtg_comm_destroy(rtg_comm* comm);
+
+/* Gather the interleaved shards of a `height`-row image of `row_bytes`-byte rows onto rank
+ * `root`. shards[i] (device memory of the i-th local rank) holds ceil(height/nranks) rows:
+ * image rows rank, rank+nranks, ... then padding. out: device memory on root's device, height
+ * rows in image order (ignored by processes without the root). streams[i] (hipStream_t, may be
+ * NULL = the communicator's own) orders the gather after the render that filled shards[i].
+ * Asynchronous: returns once enqueued (every local rank's part, one RCCL group). */
+rtg_status rtg_gather_rows(rtg_comm* comm, const void* const* shards, int32_t height, int64_t row_bytes,
+                           int32_t root, void* out, void* const* streams);
+
+/* The de-interleave step of rtg_gather_rows on its own: `gathered` holds nranks blocks of
+ * ceil(height/nranks) rows (block r = rank r's shard); writes image row r + k*nranks from row k of
+ * block r. Device memory on `device`; asynchronous on `stream`. */
+rtg_status rtg_deinterleave_rows(int32_t device, const void* gathered, void* out, int32_t nranks,
+                                 int32_t height, int64_t row_bytes, void* stream);
+
+/* A whole multi-GPU frame for the C++ mirror's camera (camera.devices): scenes[i] is the scene on
+ * the i-th local rank's device; each renders its interleaved rows into device memory, the frame is
+ * gathered to `root` over RCCL and copied to out_rgb (host, H*W*3 floats, on the root's process).
+ * stats: segments / samples summed over the local ranks, kernel_ms the slowest rank's. */
+rtg_status rtg_render_frame(rtg_comm* comm, rtg_scene* const* scenes, const rtg_camera_desc* cam,
+                            uint64_t seed, int32_t root, float* out_rgb, rtg_render_stats* stats);
 
 /* Host-only: build the BVH the scene would use and report its topology (no GPU needed).
  * nodes_out (optional, capacity max_nodes) receives per node: {left, right} child codes

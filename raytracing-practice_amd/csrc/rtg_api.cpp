@@ -22,6 +22,7 @@ hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, in
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
                          bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream);
 int lds_layout(const DevScene& S, int stack, int waves, DevJob* J);
+int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J);
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
 }  // namespace rtg
 
@@ -167,6 +168,8 @@ bool validate_texture(const rtg_scene_desc* d, int32_t tex, int depth, std::stri
 
 namespace rtg {
 
+rtg_status set_last_error(rtg_status code, const std::string& msg) { return fail(code, msg); }
+
 void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
   // camera::initialize (camera.hpp:76-136), fp64 with the reference's float-literal quirks.
   const double pi = 3.1415926535897932385;
@@ -299,6 +302,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->stack_need = 0;
   } else if (d->bvh_mode == RTG_BVH_SAH && !bvh.nodes.empty()) {
     collapse_bvh4(bvh, &bvh4);
+    reorder_top_bfs(&bvh4, kTreeletBfsNodes);
     out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
     out->depth = bvh4.depth;
     out->stack_need = bvh4.max_pushes;
@@ -737,6 +741,9 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.num_nodes = hs.num_nodes;
   s->dev.root_code = 0;
   s->dev.occluder = hs.occluder;
+  s->dev.sphere_f4 = 2;
+  s->dev.treelet_bytes = 0;  // set per render by the treelet schedule
+  s->dev.treelet_lds = 0;
   s->dev.node_limit = static_cast<int32_t>(std::min<int64_t>(hs.num_nodes * 112, INT32_MAX));
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
@@ -930,16 +937,25 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   // most its occupancy allows), deeper BVHs spill the rest to a global per-wave area; the A/B
   // schedules 1 and 2 keep the whole stack in LDS.
   const int need = std::max(1, s->stack_need);
-  const int lds_bytes = lds_layout(s->dev, kLdsStack, kLdsWaves, &dj);
-  if (variant == 0) variant = lds_bytes > 0 ? 3 : 4;
-  if (variant == 5) variant = 3;  // former 16-wave alias
+  DevScene dscene = s->dev;  // this render's view (the treelet schedule sets its LDS part)
+  dj.lds_sphere_f4 = 3;      // 48-B sphere records in LDS (bank spread)
+  if (const char* e = std::getenv("RTG_LDS_SPHERE_F4")) dj.lds_sphere_f4 = std::atoi(e) == 2 ? 2 : 3;  // A/B
+  int lds_bytes = lds_layout(dscene, kLdsStack, kLdsWaves, &dj);
+  // default: the whole scene in LDS (3); else the top of a 4-wide tree in LDS (5, config 5's 1M
+  // spheres: -1.3 % against 4, profiles/r02_ab), else the plain grid (4)
+  if (variant == 0) variant = lds_bytes > 0 ? 3 : (dscene.node_width == 4 ? 5 : 4);
+  if (variant == 5) {  // persistent workgroups with the top of the tree in LDS (4-wide trees)
+    if (dscene.node_width != 4) return fail(RTG_E_INVALID, "schedule 5 needs a 4-wide BVH (RTG_BVH_SAH)");
+    lds_bytes = lds_layout_treelet(&dscene, kLdsStack, kLdsWaves, &dj);
+    if (lds_bytes < 0) return fail(RTG_E_INVALID, "schedule 5: no LDS room for the treelet");
+  }
   if (variant == 4) variant = 0;  // plain-grid ballot schedule
   if (variant == 3 && lds_bytes < 0) return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
   if ((variant == 1 || variant == 2) && s->dev.node_width != 2)
     return fail(RTG_E_INVALID, "schedules 1 and 2 need a binary BVH (RTG_BVH_MEDIAN)");
   int stack_depth = 0;
   int grid_blocks = 1, grid_waves = 0;
-  if (variant == 3) {
+  if (variant == 3 || variant == 5) {
     stack_depth = kLdsStack;
     grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
     grid_waves = grid_blocks * kLdsWaves;
@@ -956,7 +972,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   // RTG_STACK_LDS_ENTRIES (tests): keep fewer entries in LDS so the global spill path is exercised
   if (const char* e = std::getenv("RTG_STACK_LDS_ENTRIES"))
     dj.lds_stack = std::min(stack_depth, std::max(1, std::atoi(e)));
-  dj.spill_depth = (variant == 3 || variant == 0) ? std::max(0, need - dj.lds_stack) : 0;
+  const bool default_sched = variant == 3 || variant == 0 || variant == 5;  // the ballot-batched stream
+  dj.spill_depth = default_sched ? std::max(0, need - dj.lds_stack) : 0;
   dj.spill = nullptr;
   StreamScratch scratch;
   scratch.stream = stream;
@@ -971,20 +988,20 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const char* trace_path = std::getenv("RTG_WAVE_TRACE");
   int64_t trace_slots = 0;
   if (trace_path) {
-    trace_slots = variant == 3 || variant == 0 ? int64_t(grid_waves)
+    trace_slots = default_sched ? int64_t(grid_waves)
                                                : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
     RTG_HIP(hipMallocAsync(scratch.add(), trace_slots * 32, stream), "hipMalloc(trace)");
     dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
   }
-  if (progressive && !(variant == 3 || variant == 0))
+  if (progressive && !default_sched)
     return fail(RTG_E_INVALID, "progressive rendering needs the default schedules");
-  const bool chunked = !progressive && dj.chunks > 1 && (variant == 3 || variant == 0) && dc.max_depth > 0;
+  const bool chunked = !progressive && dj.chunks > 1 && default_sched && dc.max_depth > 0;
   if (chunked) {
     RTG_HIP(hipMallocAsync(scratch.add(), out_bytes * dj.chunks, stream), "hipMallocAsync(partial sums)");
     dj.partial = static_cast<float*>(scratch.ptr[scratch.n - 1]);
   }
-  if (!(variant == 3 || variant == 0)) {  // schedules 1 and 2 keep one running sum per pixel
+  if (!default_sched) {  // schedules 1 and 2 keep one running sum per pixel
     dj.chunks = 1;
     dj.chunk_samples = std::max(1, cam->samples_per_pixel);
   }
@@ -995,7 +1012,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
             "hipMemsetAsync(partial sums)");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
   if (!skip_kernel)
-    RTG_HIP(launch_render(s->dev, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
+    RTG_HIP(launch_render(dscene, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
                           variant, lds_bytes, grid_blocks, stream),
             "render kernel launch");
   if (chunked || (progressive && dout))

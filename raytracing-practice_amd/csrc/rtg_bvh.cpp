@@ -380,6 +380,37 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
   rec.fill(0, 0, 1, 0);
 }
 
+void reorder_top_bfs(Bvh4* t, int64_t top) {
+  const int64_t n = static_cast<int64_t>(t->nodes.size());
+  if (n <= 1 || top <= 1) return;
+  // the first `top` nodes of a breadth-first walk from the root, then the rest in their (depth-first)
+  // order; a node's inner children stay next to each other in both parts
+  std::vector<int32_t> order;
+  order.reserve(n);
+  std::vector<char> taken(n, 0);
+  order.push_back(0);
+  taken[0] = 1;
+  for (size_t head = 0; head < order.size() && static_cast<int64_t>(order.size()) < top; ++head)
+    for (int c = 0; c < 4 && static_cast<int64_t>(order.size()) < top; ++c) {
+      const int32_t ch = t->nodes[order[head]].child[c];
+      if (ch >= 0 && !taken[ch]) {
+        taken[ch] = 1;
+        order.push_back(ch);
+      }
+    }
+  for (int32_t k = 0; k < n; ++k)
+    if (!taken[k]) order.push_back(k);
+  std::vector<int32_t> pos(n);
+  for (int32_t k = 0; k < n; ++k) pos[order[k]] = k;
+  std::vector<BuildNode4> out(n);
+  for (int32_t k = 0; k < n; ++k) {
+    out[k] = t->nodes[order[k]];
+    for (int c = 0; c < 4; ++c)
+      if (out[k].child[c] >= 0) out[k].child[c] = pos[out[k].child[c]];
+  }
+  t->nodes.swap(out);
+}
+
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
   out->nodes.clear();
   out->refs.clear();

@@ -79,6 +79,12 @@ struct Bvh4 {
 // until four slots are filled); leaf codes and refs are unchanged.
 void collapse_bvh4(const Bvh& bin, Bvh4* out);
 
+// Renumber a 4-wide tree so its first `top` nodes are the top of the tree in breadth-first order
+// (the root stays node 0; the rest keep their depth-first order). Scenes too large for LDS keep
+// that prefix in LDS (the treelet schedule), so the nodes every ray visits are ds_reads.
+constexpr int64_t kTreeletBfsNodes = 4096;
+void reorder_top_bfs(Bvh4* t, int64_t top);
+
 // aabb of one primitive exactly as the reference computes it (aabb.hpp:30-48,135-154;
 // sphere.hpp:16-44; quad.hpp:30-38).
 void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]);
@@ -86,6 +92,8 @@ void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]);
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err);
 bool compile_scene(const rtg_scene_desc* desc, HostScene* out, std::string* err);
 void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* out);
+// rtg_last_error() text of the calling thread; returns `code` (rtg_api.cpp)
+rtg_status set_last_error(rtg_status code, const std::string& msg);
 
 // Kernel-side camera / job parameters (passed by value to the kernels).
 struct DevCamera {
@@ -135,6 +143,11 @@ struct DevScene {
   // a sphere whose box spans most of the scene (book-1's ground) is kept out of the BVH and tested
   // by every ray before its traversal, in the shading phase (sphere index, -1: none)
   int32_t occluder;
+  // treelet schedule: inner-node codes below this byte offset are read from the LDS copy of the
+  // first nodes (the breadth-first top of the tree), the others from HBM / caches
+  int32_t treelet_bytes;
+  uint32_t treelet_lds;  // LDS byte address of that copy (set inside the kernel)
+  int32_t sphere_f4;     // float4s per sphere record: 2 in HBM, DevJob::lds_sphere_f4 in the LDS copy
 };
 
 struct GpuBvhResult {  // rtg_gpubvh.hip
@@ -175,6 +188,7 @@ struct DevJob {
   // persistent LDS kernel: byte offsets of the scene copies in dynamic LDS
   int32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_materials, lds_textures;
   int32_t lds_perlin_vec, lds_perlin_perm;  // noise tables (full-texture kernels only)
+  int32_t lds_sphere_f4;                     // float4s per sphere record in the LDS copy (2 or 3)
 
 };
 

@@ -19,6 +19,7 @@
 // Numerics: the fp32 spec in DESIGN.md ("rtg-f32"); compiled with -ffp-contract=off so every
 // expression rounds as written and matches the CPU restatement in oracle/cpu_ref.c. The only
 // fused ops are the slab tests, which only cull (boxes are rounded outward on the host).
+#include <algorithm>
 #include <cstdint>
 
 #include "rtg_internal.hpp"
@@ -348,9 +349,17 @@ __device__ __forceinline__ void usort(uint32_t& a, uint32_t& b) {
 // far-to-near. Empty slots hold the inverted box (+inf, -inf): whatever the signs, at least one
 // axis has a finite 1/d, for which the near plane gives tn = +inf and the far one tf = -inf, so an
 // empty slot can never be entered (rays with all three components zero do not exist).
-template <class Stk, bool COUNT, bool PAIRS>
+// Node geometry of a schedule: where node rows are read from.
+enum Geom : int {
+  kGeomLds = 0,      // whole scene in LDS; inner codes are absolute LDS addresses, codes read after the sort
+  kGeomGlobal = 1,   // scene through the caches; codes travel with their keys through the sort network
+  kGeomTreelet = 2,  // nodes below S.treelet_bytes from their LDS copy, the rest through the caches
+};
+
+template <class Stk, bool COUNT, int GEOM>
 __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
+  constexpr bool PAIRS = GEOM != kGeomLds;
   // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
   if (t.todo >= S.node_limit) {
     corrupt = true;
@@ -360,12 +369,25 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
   const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
   const uint32_t na = static_cast<uint32_t>(t.todo);  // LDS scenes: the node's LDS address
-  auto row = [&](int32_t off) -> nf4 {
-    if constexpr (PAIRS) return *reinterpret_cast<const nf4*>(nb + off);
-    else return lds_ld4(na + static_cast<uint32_t>(off));
-  };
-  const nf4 nx = row(sx), ny = row(16 + sy), nz = row(32 + sz);
-  const nf4 fx = row(48 - sx), fy = row(64 - sy), fz = row(80 - sz);
+  nf4 nx, ny, nz, fx, fy, fz;
+  int4 cc;
+  if constexpr (GEOM == kGeomLds) {
+    nx = lds_ld4(na + sx), ny = lds_ld4(na + 16 + sy), nz = lds_ld4(na + 32 + sz);
+    fx = lds_ld4(na + 48 - sx), fy = lds_ld4(na + 64 - sy), fz = lds_ld4(na + 80 - sz);
+  } else {
+    if (GEOM == kGeomTreelet && t.todo < S.treelet_bytes) {  // the top of the tree: a ds_read
+      const uint32_t la = S.treelet_lds + na;
+      nx = lds_ld4(la + sx), ny = lds_ld4(la + 16 + sy), nz = lds_ld4(la + 32 + sz);
+      fx = lds_ld4(la + 48 - sx), fy = lds_ld4(la + 64 - sy), fz = lds_ld4(la + 80 - sz);
+      const nf4 c4 = lds_ld4(la + 96);
+      cc = *reinterpret_cast<const int4*>(&c4);
+    } else {
+      auto row = [&](int32_t off) -> nf4 { return *reinterpret_cast<const nf4*>(nb + off); };
+      nx = row(sx), ny = row(16 + sy), nz = row(32 + sz);
+      fx = row(48 - sx), fy = row(64 - sy), fz = row(80 - sz);
+      cc = *reinterpret_cast<const int4*>(nb + 96);
+    }
+  }
   if (COUNT) cnt.box += 4;
   const f2 ix = {t.ix, t.ix}, iy = {t.iy, t.iy}, iz = {t.iz, t.iz};
   const f2 ox = {t.ox, t.ox}, oy = {t.oy, t.oy}, oz = {t.oz, t.oz};
@@ -383,7 +405,6 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
     // scene in global memory: the codes travel with their keys through the network, so no second
     // memory round trip sits between the sort and the next node load (-3.6 % on config 5; with
     // the scene in LDS the extra selects cost more than the LDS latency they save)
-    const int4 cc = *reinterpret_cast<const int4*>(nb + 96);
     int32_t c0 = cc.x, c1 = cc.y, c2 = cc.z, c3 = cc.w;
     psort(k0, c0, k1, c1);
     psort(k2, c2, k3, c3);
@@ -444,7 +465,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
   }
   if (S.ref_mode == 1) {  // sphere-only scene, primitives stored in reference order
     for (int k = 0; k < count; ++k) {
-      const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * 2;
+      const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
       if (th > 0.0f) {
@@ -463,7 +484,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       th = ref == t.origin ? -1.0f
                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, t.tbest);
     } else {
-      const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
+      const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
     }
     if (th > 0.0f) {  // th > tmin >= 0.001 on a hit
@@ -560,7 +581,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
           t = ref == origin ? -1.0f
                             : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest);
         } else {
-          const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * 2;
+          const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
           t = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
         }
         if (t > 0.0f) {  // t > tmin >= 0.001 on a hit
@@ -718,7 +739,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   int mat;
   bool sphere = !(ref & kQuadRefBit);
   if (sphere) {
-    const float4* s = S.spheres + static_cast<int64_t>(ref) * 2;
+    const float4* s = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
     const float4 s0 = s[0], s1 = s[1];
     const V3 C = v3(s0.x + ps.time * s1.x, s0.y + ps.time * s1.y, s0.z + ps.time * s1.z);
     p = add(ps.o, scl(t, ps.d));
@@ -916,7 +937,7 @@ __device__ __forceinline__ void start_pixel_sample(PathState& ps, const DevCamer
 // or a leaf step for the whole wave (leaf work waits until leaf_batch lanes have reached a leaf);
 // the wave switches to shading once ceil(alive * shade_batch / 64) lanes have finished their
 // closest-hit query, and lanes still traversing keep their stack and continue afterwards.
-template <class Stk, bool COUNT, int WIDE, bool TEXF, bool GLOBAL_SCENE>
+template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM>
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
                                               const Stk& stk, WaveStats<COUNT>& w) {
   const int lane = __lane_id();
@@ -987,7 +1008,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     if (fresh || cont) {
       trav_begin(tr, S, ps.o, ps.d, ps.origin);
       if (S.occluder >= 0) {  // the scene-spanning sphere kept out of the BVH (DevScene::occluder)
-        const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * 2;
+        const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * S.sphere_f4;
         if (COUNT) w.cnt.prim += 1;
         const float th = sphere_t(sp4[0], sp4[1], ps.o, ps.d, tr.a, tr.inv_a, ps.time, kTMin, tr.tbest,
                                   S.occluder == ps.origin);
@@ -1029,7 +1050,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       if (tr.active && tr.todo >= 0) {
         if constexpr (WIDE == 4)
-          node_step4<Stk, COUNT, GLOBAL_SCENE>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+          node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
         else
           node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
       }
@@ -1104,9 +1125,9 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   if constexpr (SPILL) {
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, true>(S, C, J, stk, w);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal>(S, C, J, stk, w);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, true>(S, C, J, LdsStack<STACK>{lstk}, w);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal>(S, C, J, LdsStack<STACK>{lstk}, w);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, slot, (blockIdx.x << 8) | wave);
@@ -1117,13 +1138,39 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
 // L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
 // left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF>
+//
+// GEOM = kGeomTreelet (schedule 5, scenes too large for LDS such as the 1M-sphere field): the same
+// persistent workgroups keep only the breadth-first top of the 4-wide tree in LDS (as many nodes as
+// fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
+// through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM>
 __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int32_t* lstk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
+  if constexpr (GEOM == kGeomTreelet) {
+    float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
+    for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += WAVES * 64) l_top[k] = S.nodes[k];
+    __syncthreads();
+    DevScene L = S;
+    L.treelet_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                        (__attribute__((address_space(3))) unsigned char*)smem)) +
+                    static_cast<uint32_t>(J.lds_nodes);
+    WaveStats<COUNT> w;
+    if constexpr (SPILL) {
+      const int slot = blockIdx.x * WAVES + wave;
+      const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
+                                  J.lds_stack, J.lds_stack + J.spill_depth};
+      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet>(L, C, J, stk, w);
+    } else {
+      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet>(L, C, J, LdsStack<STACK>{lstk}, w);
+    }
+    flush_stats<COUNT>(J, w, lane);
+    trace_wave(J, t0, w.pixels, lane, blockIdx.x * WAVES + wave, (blockIdx.x << 8) | wave);
+    return;
+  }
   float4* l_nodes = reinterpret_cast<float4*>(smem + J.lds_nodes);
   int32_t* l_refs = reinterpret_cast<int32_t*>(smem + J.lds_refs);
   float4* l_spheres = reinterpret_cast<float4*>(smem + J.lds_spheres);
@@ -1147,7 +1194,10 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
     }
     l_nodes[k] = v;
   }
-  for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64) l_spheres[k] = S.spheres[k];
+  // sphere records padded to J.lds_sphere_f4 float4s in LDS (3: 48-B stride, an odd number of 16-B
+  // bank slots, so the ds_read_b128 of 16 lanes at different spheres spread over all 16 slots)
+  for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64)
+    l_spheres[(k >> 1) * J.lds_sphere_f4 + (k & 1)] = S.spheres[k];
   for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
   if (S.ref_mode == 0)
     for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
@@ -1166,6 +1216,7 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
   }
   L.refs = l_refs;
   L.spheres = l_spheres;
+  L.sphere_f4 = J.lds_sphere_f4;
   L.quads = l_quads;
   L.materials = l_materials;
   L.textures = l_textures;
@@ -1178,9 +1229,9 @@ __global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevC
     const int slot = blockIdx.x * WAVES + wave;
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, false>(L, C, J, stk, w);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, stk, w);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, false>(L, C, J, LdsStack<STACK>{lstk}, w);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, LdsStack<STACK>{lstk}, w);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, blockIdx.x * WAVES + wave, (blockIdx.x << 8) | wave);
@@ -1326,20 +1377,32 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
-template <int STACK, bool SPILL, int WIDE, bool TEXF>
+template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds>
 hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                       int lds_bytes, int grid_blocks, hipStream_t stream) {
-  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF>);
+  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF, GEOM>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF, GEOM>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (count)
-    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
+    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF, GEOM>), dim3(grid_blocks),
                        dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF>), dim3(grid_blocks),
+    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF, GEOM>), dim3(grid_blocks),
                        dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
   return hipGetLastError();
+}
+
+// Schedule 5: the persistent kernel with an LDS treelet over a scene in HBM (4-wide trees only).
+hipError_t launch_treelet(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int lds_bytes,
+                          int grid_blocks, hipStream_t stream) {
+  if (S.node_width != 4 || J.lds_stack > kLdsStack) return hipErrorInvalidValue;
+  const bool spill = J.spill_depth > 0, tex = S.tex_full != 0;
+  if (spill)
+    return tex ? launch_lds<kLdsStack, true, 4, true, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream)
+               : launch_lds<kLdsStack, true, 4, false, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream);
+  return tex ? launch_lds<kLdsStack, false, 4, true, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream)
+             : launch_lds<kLdsStack, false, 4, false, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream);
 }
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF>
@@ -1416,7 +1479,7 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
   const int64_t nodes = off;
   off = a16(off + S.num_nodes * (S.node_width == 4 ? 112 : 64));
   const int64_t spheres = off;
-  off = a16(off + S.num_spheres * 32);
+  off = a16(off + S.num_spheres * 16 * (J ? J->lds_sphere_f4 : 3));
   const int64_t quads = off;
   off = a16(off + S.num_quads * 80);
   const int64_t refs = off;
@@ -1443,9 +1506,22 @@ int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
   return static_cast<int>(off);
 }
 
+// Dynamic LDS of the treelet schedule: the stacks, then as many of the first (breadth-first) 4-wide
+// nodes as fit in the rest of one CU's 160 KiB; sets S.treelet_bytes and J.lds_nodes.
+int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
+  const int64_t stacks = int64_t(waves) * stack * 64 * 4;
+  const int64_t room = 160 * 1024 - stacks;
+  if (S->node_width != 4 || room < 112) return -1;
+  const int64_t nodes = std::min<int64_t>(S->num_nodes, room / 112);
+  S->treelet_bytes = static_cast<int32_t>(nodes * 112);
+  J->lds_nodes = static_cast<int32_t>(stacks);
+  return static_cast<int>(stacks + nodes * 112);
+}
+
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
                          bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
   if (J.row_count <= 0 || C.width <= 0) return hipSuccess;
+  if (variant == 5) return launch_treelet(S, C, J, count, lds_bytes, grid_blocks, stream);
   if (variant == 3 || variant == 0)
     return S.node_width == 4 ? launch_default<4>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream)
                              : launch_default<2>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream);

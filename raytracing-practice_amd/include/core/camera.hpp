@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <exception>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -70,7 +71,9 @@ class camera {
   // ---- extensions (not in the reference) ----
   uint64_t seed = 0x5EED;          // counter-RNG run seed
   int device = 0;                  // HIP device to render on
-  std::vector<int> devices;        // > 1 entries: row-interleaved shards on these devices (threads)
+  // row-interleaved shards on these devices, gathered over RCCL (rtg_render_frame); a device listed
+  // twice (tests on a one-GPU box: RCCL takes one rank per device) renders from host threads instead
+  std::vector<int> devices;
   int bvh_mode = RTG_BVH_SAH;      // device BVH builder
   rtg_render_stats last_stats{};   // segments, samples, kernel time of the last render
 
@@ -85,9 +88,40 @@ class camera {
 
   // The linear, pre-gamma per-pixel mean (what the reference hands to write_color), H*W*3.
   std::vector<float> render_linear(const hittable& world) {
-    if (devices.size() > 1) return render_linear_multi(world);
+    if (!devices.empty()) {
+      std::vector<int> sorted(devices);
+      std::sort(sorted.begin(), sorted.end());
+      if (std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end()) return render_linear_rccl(world);
+      return render_linear_multi(world);
+    }
     rtgpu::device_scene scene(world, device, bvh_mode);
     return render_linear(scene);
+  }
+
+  // One scene per device, rows r, r+N, ... on device r, one RCCL gather to devices[0] and the
+  // de-interleave there (rtg_render_frame), then the frame to the host.
+  std::vector<float> render_linear_rccl(const hittable& world) {
+    rtgpu::scene_builder sb;
+    rtgpu::device_scene::flatten(world, sb);
+    const rtg_scene_desc d = sb.desc(bvh_mode);
+    const rtg_camera_desc cd = desc();
+    const std::vector<int32_t> devs(devices.begin(), devices.end());
+    std::vector<std::unique_ptr<rtgpu::device_scene>> scenes;
+    std::vector<rtg_scene*> handles;
+    for (int32_t dv : devs) {
+      scenes.emplace_back(new rtgpu::device_scene(d, dv));
+      handles.push_back(scenes.back()->handle());
+    }
+    rtg_comm* comm = nullptr;
+    rtgpu::check(rtg_comm_create_local(devs.data(), static_cast<int32_t>(devs.size()), &comm),
+                 "rtg_comm_create_local");
+    std::vector<float> rgb(static_cast<size_t>(image_height()) * image_width * 3);
+    const rtg_status st = rtg_render_frame(comm, handles.data(), &cd, seed, 0, rgb.data(), &last_stats);
+    const std::string err = st == RTG_OK ? std::string() : std::string(rtg_last_error());
+    rtg_comm_destroy(comm);
+    if (st != RTG_OK)
+      throw std::runtime_error("rtgpu: rtg_render_frame failed (" + std::to_string(st) + "): " + err);
+    return rgb;
   }
 
   // write_color (color.hpp:26-58) for every pixel, the text formatted on all host cores and
@@ -118,8 +152,9 @@ class camera {
     for (const std::string& s : text) out.write(s.data(), static_cast<std::streamsize>(s.size()));
   }
 
-  // One host thread per entry of `devices`: device r renders rows r, r+N, ... (the RNG is keyed
-  // by the global pixel, so the frame is identical to a single-device render).
+  // One host thread per entry of `devices` (used when a device is listed twice): device r renders
+  // rows r, r+N, ... into host memory (the RNG is keyed by the global pixel, so the frame is
+  // identical to a single-device render).
   std::vector<float> render_linear_multi(const hittable& world) {
     rtgpu::scene_builder sb;
     rtgpu::device_scene::flatten(world, sb);

@@ -123,7 +123,10 @@ class rts_params(C.Structure):
 # exported symbols of librtgpu.so (must match include/rtgpu.h)
 RTG_SYMBOLS = ("rtg_abi_version", "rtg_last_error", "rtg_device_count", "rtg_camera_resolve",
                "rtg_scene_create", "rtg_scene_get_info", "rtg_scene_destroy", "rtg_render",
-               "rtg_render_wait", "rtg_resolve_rgb8", "rtg_bvh_build_host")
+               "rtg_render_wait", "rtg_resolve_rgb8", "rtg_bvh_build_host", "rtg_comm_create_local",
+               "rtg_comm_unique_id", "rtg_comm_create_rank", "rtg_comm_size", "rtg_comm_destroy",
+               "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame")
+RTG_COMM_ID_BYTES = 128
 
 
 class RtgError(RuntimeError):
@@ -172,9 +175,23 @@ class Library:
         L.rtg_bvh_build_host.argtypes = [_P(rtg_scene_desc), _P(rtg_bvh_node_host), C.c_int64,
                                          _P(C.c_int64), C.c_int64, _P(C.c_int64), _P(C.c_int64),
                                          _P(C.c_int32)]
+        L.rtg_comm_create_local.argtypes = [_P(C.c_int32), C.c_int32, _P(C.c_void_p)]
+        L.rtg_comm_unique_id.argtypes = [C.c_void_p]
+        L.rtg_comm_create_rank.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _P(C.c_void_p)]
+        L.rtg_comm_size.argtypes = [C.c_void_p, _P(C.c_int32), _P(C.c_int32)]
+        L.rtg_comm_destroy.argtypes = [C.c_void_p]
+        L.rtg_comm_destroy.restype = None
+        L.rtg_gather_rows.argtypes = [C.c_void_p, _P(C.c_void_p), C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
+                                      _P(C.c_void_p)]
+        L.rtg_deinterleave_rows.argtypes = [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64,
+                                            C.c_void_p]
+        L.rtg_render_frame.argtypes = [C.c_void_p, _P(C.c_void_p), _P(rtg_camera_desc), C.c_uint64, C.c_int32,
+                                       C.c_void_p, _P(rtg_render_stats)]
         for name in ("rtg_device_count", "rtg_camera_resolve", "rtg_scene_create",
                      "rtg_scene_get_info", "rtg_render", "rtg_render_wait", "rtg_resolve_rgb8",
-                     "rtg_bvh_build_host"):
+                     "rtg_bvh_build_host", "rtg_comm_create_local", "rtg_comm_unique_id",
+                     "rtg_comm_create_rank", "rtg_comm_size", "rtg_gather_rows", "rtg_deinterleave_rows",
+                     "rtg_render_frame"):
             getattr(L, name).restype = C.c_int32
         if L.rtg_abi_version() != RTG_ABI_VERSION:
             raise RuntimeError("librtgpu ABI version mismatch")
@@ -208,6 +225,80 @@ class Library:
         h = C.c_void_p()
         self.check("rtg_scene_create", self.lib.rtg_scene_create(C.byref(desc), device, C.byref(h)))
         return DeviceScene(self, h)
+
+    # ---- multi-GPU frames (rtgpu.h: rtg_comm_*, rtg_gather_rows, rtg_render_frame) ----
+    def comm_local(self, devices: Sequence[int]) -> "Comm":
+        """One process driving `devices` (ranks 0..N-1), ncclCommInitAll."""
+        arr = (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        self.check("rtg_comm_create_local", self.lib.rtg_comm_create_local(arr, len(devices), C.byref(h)))
+        return Comm(self, h)
+
+    def comm_unique_id(self) -> bytes:
+        buf = (C.c_uint8 * RTG_COMM_ID_BYTES)()
+        self.check("rtg_comm_unique_id", self.lib.rtg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_rank(self, uid: bytes, nranks: int, rank: int, device: int) -> "Comm":
+        """One rank of a one-process-per-GPU communicator (uid from comm_unique_id on rank 0)."""
+        buf = (C.c_uint8 * RTG_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        self.check("rtg_comm_create_rank", self.lib.rtg_comm_create_rank(buf, nranks, rank, device, C.byref(h)))
+        return Comm(self, h)
+
+    def deinterleave_rows(self, device: int, gathered_ptr: int, out_ptr: int, nranks: int, height: int,
+                          row_bytes: int, stream_ptr: Optional[int] = None) -> None:
+        self.check("rtg_deinterleave_rows", self.lib.rtg_deinterleave_rows(
+            device, C.c_void_p(gathered_ptr), C.c_void_p(out_ptr), nranks, height, row_bytes,
+            C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
+class Comm:
+    """rtg_comm*: RCCL communicator over the GPUs a frame is tiled across."""
+
+    def __init__(self, lib: Library, handle: C.c_void_p):
+        self.L = lib
+        self.handle = handle
+
+    def size(self):
+        n, nl = C.c_int32(0), C.c_int32(0)
+        self.L.check("rtg_comm_size", self.L.lib.rtg_comm_size(self.handle, C.byref(n), C.byref(nl)))
+        return n.value, nl.value
+
+    def gather_rows(self, shard_ptrs: Sequence[int], height: int, row_bytes: int, root: int, out_ptr: int,
+                    stream_ptrs: Optional[Sequence[int]] = None) -> None:
+        """Enqueue the RCCL gather of this process's shards (device pointers, one per local rank)
+        and the de-interleave into out_ptr on the root (asynchronous on the given streams)."""
+        n = len(shard_ptrs)
+        sh = (C.c_void_p * n)(*shard_ptrs)
+        st = (C.c_void_p * n)(*(stream_ptrs or [0] * n))
+        self.L.check("rtg_gather_rows", self.L.lib.rtg_gather_rows(self.handle, sh, height, row_bytes, root,
+                                                                    C.c_void_p(out_ptr), st))
+
+    def render_frame(self, scenes: Sequence["DeviceScene"], cam: rtg_camera_desc, seed: int = DEFAULT_SEED,
+                     root: int = 0):
+        """Whole frame over the communicator's local GPUs (rtg_render_frame): (H, W, 3) on the root."""
+        import numpy as np
+
+        p = self.L.camera_resolve(cam)
+        out = np.zeros((p.image_height, p.image_width, 3), dtype=np.float32)
+        arr = (C.c_void_p * len(scenes))(*[s.handle.value if isinstance(s.handle, C.c_void_p) else s.handle
+                                           for s in scenes])
+        stats = rtg_render_stats()
+        self.L.check("rtg_render_frame", self.L.lib.rtg_render_frame(self.handle, arr, C.byref(cam), seed, root,
+                                                                      out.ctypes.data, C.byref(stats)))
+        return out, stats
+
+    def close(self) -> None:
+        if self.handle:
+            self.L.lib.rtg_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class DeviceScene:

@@ -161,6 +161,41 @@ def test_schedules_give_identical_frames(gpu_lib, scenes):
     assert max(segs) - min(segs) <= 2
 
 
+@pytest.mark.parametrize("grid,W", [(11, 96), (500, 128)])
+def test_treelet_schedule_matches_default(gpu_lib, scenes, oracle, grid, W, monkeypatch):
+    """Schedule 5 (persistent workgroups, the breadth-first top of the 4-wide tree in LDS, the rest
+    and every primitive through the caches; the default for scenes too large for LDS): book-1 (the
+    whole tree fits the treelet) and the 1M-sphere scene (the treelet holds the top ~870 of ~330k
+    nodes, the stack spills past 16 entries) render the plain grid's (schedule 4) frame and segment
+    count; also with 3 LDS stack entries."""
+    import ctypes as C
+
+    s = scenes.build("bouncing_spheres", grid=grid, rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.aspect_ratio, c.samples_per_pixel, c.max_depth = W, 16.0 / 9.0, 4, 50
+    ds = gpu_lib.scene_create(s.desc)
+    H = gpu_lib.camera_resolve(c).image_height
+    ref = np.zeros((H, W, 3), dtype=np.float32)
+    rst = rtgpu.rtg_render_stats()
+    job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, 0, 1, 0, rtgpu.RTG_RENDER_SCHEDULE(4), None)
+    gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job),
+                                                        ref.ctypes.data, C.byref(rst)))
+    default, dst = ds.render_host(c)
+    assert np.array_equal(default, ref) and dst.segments == rst.segments
+    for entries in (None, "3"):
+        if entries:
+            monkeypatch.setenv("RTG_STACK_LDS_ENTRIES", entries)
+        out = np.zeros((H, W, 3), dtype=np.float32)
+        job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, 0, 1, 0, rtgpu.RTG_RENDER_SCHEDULE(5), None)
+        st = rtgpu.rtg_render_stats()
+        gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job),
+                                                            out.ctypes.data, C.byref(st)))
+        assert np.array_equal(out, ref) and st.segments == rst.segments, entries
+    ds.close()
+    o, segs = oracle.render_f32(s.desc, c)
+    assert_parity(ref, o, rst, segs)
+
+
 def test_repeated_host_renders_are_identical(gpu_lib, scenes):
     """Host-output renders go through a scene-owned device frame and a pinned staging buffer; with
     a stream-ordered (hipMallocAsync) frame the third render of a scene came back all zero."""
@@ -565,3 +600,61 @@ def test_raytracer_cli_writes_ppm(tmp_path):
     subprocess.run([exe, str(out2), "cornell_box", "64", "8", "20", "0,0,0"], check=True, timeout=120,
                    capture_output=True)
     assert out2.read_bytes() == out.read_bytes()
+    # distinct devices: the RCCL frame path (rtg_render_frame); on a one-GPU box a world of one
+    out3 = tmp_path / "cornell3.ppm"
+    subprocess.run([exe, str(out3), "cornell_box", "64", "8", "20", "0"], check=True, timeout=120,
+                   capture_output=True)
+    assert out3.read_bytes() == out.read_bytes()
+
+
+@pytest.mark.parametrize("nranks,height,W,dtype", [(2, 37, 24, np.float32), (3, 20, 16, np.float32),
+                                                    (8, 135, 32, np.float32), (8, 9, 5, np.uint8),
+                                                    (5, 3, 64, np.uint8)])
+def test_deinterleave_kernel(gpu_lib, nranks, height, W, dtype):
+    """The root's de-interleave step of rtg_gather_rows (rtg_comm.cpp) on its own: nranks blocks of
+    ceil(H/N) padded rows -> image rows r + k*N; 16-byte path (fp32 RGB rows) and byte path (RGB8
+    rows of 15 bytes), ranks past the last row (N=5, H=3)."""
+    import torch
+
+    P = (height + nranks - 1) // nranks
+    g = torch.Generator().manual_seed(nranks * 1000 + height)
+    if dtype == np.float32:
+        blocks = torch.rand((nranks, P, W, 3), generator=g)
+    else:
+        blocks = torch.randint(0, 256, (nranks, P, W, 3), generator=g, dtype=torch.uint8)
+    dev = blocks.cuda()
+    out = torch.zeros((height, W, 3), dtype=blocks.dtype, device="cuda")
+    row_bytes = W * 3 * blocks.element_size()
+    gpu_lib.deinterleave_rows(0, dev.data_ptr(), out.data_ptr(), nranks, height, row_bytes,
+                              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    expect = rtgpu.deinterleave([b.numpy() for b in blocks], height)
+    assert np.array_equal(out.cpu().numpy(), expect)
+
+
+def test_comm_world_of_one(gpu_lib, scenes):
+    """rtg_comm at world size 1 (the one-GPU box): ncclCommInitAll / ncclCommInitRank, the RCCL
+    gather + de-interleave of a rendered shard, and rtg_render_frame == a plain render."""
+    import torch
+
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 80, 4, 20
+    ds = gpu_lib.scene_create(s.desc)
+    ref, st = ds.render_host(c, seed=11)
+    H, W = ref.shape[:2]
+    comm = gpu_lib.comm_local([0])
+    assert comm.size() == (1, 1)
+    frame, fst = comm.render_frame([ds], c, seed=11)
+    assert np.array_equal(frame, ref) and fst.segments == st.segments
+    # the gather on its own, through a one-process-per-GPU communicator of one rank
+    comm2 = gpu_lib.comm_rank(gpu_lib.comm_unique_id(), 1, 0, 0)
+    shard = torch.from_numpy(ref).cuda()
+    out = torch.zeros_like(shard)
+    stream = torch.cuda.current_stream().cuda_stream
+    comm2.gather_rows([shard.data_ptr()], H, W * 12, 0, out.data_ptr(), [stream])
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    comm2.close()
+    comm.close()
+    ds.close()

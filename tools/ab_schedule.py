@@ -67,16 +67,22 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     variants = []
+    envs = {}
     for v in a.variants.split(","):
+        # "...!K=V;K2=V2": environment variables set around this variant's renders (library A/B knobs)
+        v, env = (v.split("!", 1) if "!" in v else (v, ""))
         head, tune = (v.split("#", 1) if "#" in v else (v, ""))
         name, spec = (head.split("@", 1) if "@" in head else (first, head))
         nums = tuple(int(x) for x in (spec.split(":") + ["0", "0"])[:3])
-        variants.append((name, nums, tune))
+        variants.append((name, nums, tune, env))
+        envs[variants[-1]] = dict(kv.split("=", 1) for kv in env.split(";") if kv)
     times = {v: [] for v in variants}
     frames, segs = {}, {}
     for r in range(a.rounds):
         for v in variants:
-            name, (sched, batch, leaf), tune = v
+            name, (sched, batch, leaf), tune, _ = v
+            for k, val in envs[v].items():
+                os.environ[k] = val
             L, ds = libs[name], scene_for(name, tune)
             if "%" in tune:  # "...%v": RTG_COMBINE=v
                 os.environ["RTG_COMBINE"] = tune.split("%", 1)[1]
@@ -92,6 +98,8 @@ def main():
             st = rtgpu.rtg_render_stats()
             L.check("rtg_render", L.lib.rtg_render(ds.handle, rtgpu.C.byref(cam), rtgpu.C.byref(job),
                                                     out.data_ptr(), rtgpu.C.byref(st)))
+            for k in envs[v]:
+                os.environ.pop(k, None)
             times[v].append(st.kernel_ms)
             segs[v] = st.segments
             if r == 0:
@@ -100,7 +108,7 @@ def main():
     res = {}
     for v in variants:
         med = float(np.median(times[v]))
-        key = f"{v[0]}@" + ":".join(str(x) for x in v[1]) + (f"#{v[2]}" if v[2] else "")
+        key = f"{v[0]}@" + ":".join(str(x) for x in v[1]) + (f"#{v[2]}" if v[2] else "") + (f"!{v[3]}" if v[3] else "")
         res[key] = {"kernel_ms": [round(t, 2) for t in times[v]], "median_ms": round(med, 2),
                     "mrays_per_s": round(segs[v] / med / 1e3, 1), "segments": int(segs[v]),
                     "identical_frame": bool(np.array_equal(frames[v], base)),

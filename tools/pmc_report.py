@@ -49,6 +49,9 @@ def main():
                     help="use the non-counting dispatches only")
     ap.add_argument("--workload", default=None)
     ap.add_argument("--write-traffic", default=None)
+    ap.add_argument("--write-binding", default=None,
+                    help="write the binding-resource summary bench.py attaches (profiles/pmc_binding.json)")
+    ap.add_argument("--simds", type=int, default=1024, help="SIMDs of the chip (256 CUs x 4)")
     a = ap.parse_args()
     counters, info = {}, {}
     for sub in sorted(os.listdir(a.prof_dir)):
@@ -83,6 +86,16 @@ def main():
         ns = [m[3] for m in info.values()]
         out["effective_clock_ghz"] = avg["GRBM_GUI_ACTIVE"] / 8 / (sum(ns) / len(ns))
     out["dispatch"] = {k: {"vgpr": v[1], "lds": v[2], "ns": v[3]} for k, v in info.items()}
+    ns_avg = sum(m[3] for m in info.values()) / max(1, len(info))
+    if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg:
+        # wave64 VALU issue takes 2 cycles of a SIMD-32 (MI355X_MICROARCH.md constants table);
+        # kernel cycles per SIMD = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs)
+        cycles = avg["GRBM_GUI_ACTIVE"] / 8
+        out["valu_issue_frac"] = 2 * avg["SQ_INSTS_VALU"] / (a.simds * cycles)
+        if "valu_lane_utilization" in out:
+            out["useful_valu_frac"] = out["valu_issue_frac"] * out["valu_lane_utilization"]
+    if "SQ_LDS_BANK_CONFLICT" in avg and "SQ_ACTIVE_INST_LDS" in avg:
+        out["lds_bank_conflict_per_lds_cycle"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_ACTIVE_INST_LDS"])
     print(json.dumps(out, indent=1))
     if a.write_traffic and "hbm_bytes_per_launch" in out:
         with open(a.write_traffic, "w") as f:
@@ -91,6 +104,20 @@ def main():
                        "hbm_write_bytes": int(out["hbm_write_bytes"]),
                        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
                                  "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM"}, f, indent=1)
+    if a.write_binding:
+        keys = ("valu_issue_frac", "valu_lane_utilization", "useful_valu_frac", "wave_cycle_split",
+                "lds_bank_conflict_per_lds_cycle", "l2_hit_rate", "effective_clock_ghz")
+        rec = {"workload": a.workload, "kernel_ns": round(ns_avg),
+               **{k: out[k] for k in keys if k in out},
+               "vgpr": next(iter(out["dispatch"].values()))["vgpr"] if out["dispatch"] else None,
+               "source": "rocprofv3 --pmc passes of tools/profile.sh (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU, "
+                         "SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY, "
+                         "SQ_LDS_BANK_CONFLICT, SQ_ACTIVE_INST_LDS, GRBM_GUI_ACTIVE, TCC_HIT/MISS)",
+               "reading": "valu_issue_frac = 2 cycles x SQ_INSTS_VALU / (1024 SIMDs x kernel cycles); "
+                          "useful_valu_frac = that x lane utilisation: the fraction of the chip's fp32 "
+                          "lane-issue slots doing path-tracing work (DESIGN.md §6)"}
+        with open(a.write_binding, "w") as f:
+            json.dump(rec, f, indent=1)
     return 0
 
 

@@ -38,6 +38,7 @@ REF_IMAGE = "/root/reference/images/earthmap.jpg"
 HYBRID_RENDERS = [
     ("book1", 96, 54, 8, 10, 1),
     ("cornell", 40, 40, 8, 20, 3),
+    ("cornell_translate", 40, 40, 8, 100, 9),  # the reference's translate class (hittable.hpp:74-117)
     ("simple_light", 64, 36, 8, 20, 5),
     ("perlin", 64, 36, 4, 10, 7),
 ]
@@ -106,18 +107,7 @@ def main() -> int:
         json.dump(data, f, separators=(",", ":"))
     print("reference_golden.json:", {k: len(v) if isinstance(v, list) else "…" for k, v in data.items()})
 
-    for scene, W, H, spp, depth, seed in HYBRID_RENDERS:
-        with tempfile.TemporaryDirectory() as td:
-            path = os.path.join(td, "fb.bin")
-            meta = json.loads(subprocess.run(
-                [HARNESS, "render", scene, str(W), str(H), str(spp), str(depth), str(seed), path],
-                check=True, capture_output=True, text=True).stdout)
-            fb = np.fromfile(path, dtype=np.float64).reshape(meta["height"], meta["width"], 3)
-        np.savez_compressed(os.path.join(GOLDEN, f"hybrid_{scene}.npz"), fb=fb,
-                            W=W, H=H, spp=spp, depth=depth, seed=seed,
-                            segments=meta["segments"])
-        print(f"hybrid_{scene}: {fb.shape} segments={meta['segments']}")
-
+    gen_hybrid()
     gen_scene_records()
     gen_moments()
 
@@ -133,9 +123,28 @@ def main() -> int:
     return 0
 
 
+def gen_hybrid(only=None) -> None:
+    for scene, W, H, spp, depth, seed in HYBRID_RENDERS:
+        if only and scene not in only:
+            continue
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "fb.bin")
+            meta = json.loads(subprocess.run(
+                [HARNESS, "render", scene, str(W), str(H), str(spp), str(depth), str(seed), path],
+                check=True, capture_output=True, text=True).stdout)
+            fb = np.fromfile(path, dtype=np.float64).reshape(meta["height"], meta["width"], 3)
+        np.savez_compressed(os.path.join(GOLDEN, f"hybrid_{scene}.npz"), fb=fb,
+                            W=W, H=H, spp=spp, depth=depth, seed=seed,
+                            segments=meta["segments"])
+        print(f"hybrid_{scene}: {fb.shape} segments={meta['segments']}")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "moments":  # regenerate only the G5 fixtures
         gen_moments(sys.argv[2:] or None)
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "hybrid":
+        gen_hybrid(sys.argv[2:] or None)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "records":
         gen_scene_records()

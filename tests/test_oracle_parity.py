@@ -17,7 +17,7 @@ import rtgpu
 from conftest import GOLDEN
 
 SCENE_OF = {"book1": "bouncing_spheres", "cornell": "cornell_box", "simple_light": "simple_light",
-            "perlin": "perlin_sphere"}
+            "perlin": "perlin_sphere", "cornell_translate": "cornell_translate"}
 
 
 def hybrid_camera(scene, W, H, spp, depth):

@@ -190,8 +190,16 @@ struct Trav {
   int32_t todo;   // inner node (>= 0: index, or byte offset in 4-wide trees) or leaf code (< 0)
   int32_t sp;     // stack depth
   int32_t origin; // primitive ref the ray starts on (-1: camera ray), DESIGN.md §4 "origin rule"
-  bool active;    // traversal not finished
 };
+
+// todo of a finished traversal. "Traversal active" is this integer compare, not a bool of its own:
+// a bool carried around the trip loop becomes a lane mask that every ballot copies into a VGPR and
+// compares back (2 VALU per ballot); a compare of todo feeds s_bcnt1 / the exec mask directly.
+constexpr int32_t kTravDone = INT32_MAX;
+__device__ __forceinline__ bool trav_active(const Trav& t) { return t.todo != kTravDone; }
+__device__ __forceinline__ bool at_inner(const Trav& t) {  // 0 <= todo < kTravDone
+  return static_cast<uint32_t>(t.todo) < static_cast<uint32_t>(kTravDone);
+}
 
 __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d, int32_t origin) {
   t.ix = __builtin_amdgcn_rcpf(d.x);
@@ -207,10 +215,9 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.oz = -o.z * t.iz;
   t.tbest = __builtin_inff();
   t.best = -1;
-  t.todo = S.root_code;
+  t.todo = S.num_nodes > 0 ? S.root_code : kTravDone;
   t.sp = 0;
   t.origin = origin;
-  t.active = S.num_nodes > 0;
 }
 
 // Per-lane traversal stacks, laid out [depth][lane] (bank-conflict-free ds_read/write_b32).
@@ -250,7 +257,7 @@ struct SpillStack {
 template <class Stk>
 __device__ __forceinline__ void trav_pop(Trav& t, const Stk& stk) {
   if (t.sp == 0) {
-    t.active = false;
+    t.todo = kTravDone;
     return;
   }
   --t.sp;
@@ -264,7 +271,7 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, const Stk&
                                           bool& overflow, bool& corrupt) {
   if (t.todo >= S.num_nodes) {  // corrupt child code: report, never read out of bounds
     corrupt = true;
-    t.active = false;
+    t.todo = kTravDone;
     return;
   }
   const float4* n = S.nodes + static_cast<int64_t>(t.todo) * 4;
@@ -363,7 +370,7 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
   if (t.todo >= S.node_limit) {
     corrupt = true;
-    t.active = false;
+    t.todo = kTravDone;
     return;
   }
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
@@ -460,7 +467,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
   const int32_t count = (code & 7) + 1;
   if (static_cast<int64_t>(first) + count > S.num_refs) {
     corrupt = true;
-    t.active = false;
+    t.todo = kTravDone;
     return;
   }
   if (S.ref_mode == 1) {  // sphere-only scene, primitives stored in reference order
@@ -956,7 +963,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   bool exhausted = false;
   PathState ps = {};
   Trav tr = {};
-  tr.active = false;
+  tr.todo = kTravDone;
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   for (;;) {
     // hand the next units of the current batch (new batches as needed) to the lanes without one
@@ -1028,11 +1035,11 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     for (;;) {
       if (COUNT) {
         w.diag[0] += 1;
-        w.diag[1] += __popcll(ballot(tr.active));
+        w.diag[1] += __popcll(ballot(trav_active(tr)));
         w.diag[2] += __popcll(ballot(!has));
       }
-      const int at_leaf = __popcll(ballot(tr.active && tr.todo < 0));
-      const bool inner_left = ballot(tr.active && tr.todo >= 0) != 0;
+      const int at_leaf = __popcll(ballot(tr.todo < 0));
+      const bool inner_left = ballot(at_inner(tr)) != 0;
       const bool leaf_trip = at_leaf >= J.leaf_batch || !inner_left;
       uint64_t tl = 0;
       if (COUNT) {
@@ -1041,22 +1048,22 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           w.diag[10] += at_leaf;
           tl = __builtin_amdgcn_s_memtime();
         } else {
-          w.diag[9] += __popcll(ballot(tr.active && tr.todo >= 0));
+          w.diag[9] += __popcll(ballot(at_inner(tr)));
         }
       }
-      if (leaf_trip && tr.active && tr.todo < 0)
+      if (leaf_trip && tr.todo < 0)
         leaf_step<Stk, COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
-      if (tr.active && tr.todo >= 0) {
+      if (at_inner(tr)) {
         if constexpr (WIDE == 4)
           node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
         else
           node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
       }
       if (COUNT && leaf_trip) w.diag[8] += __builtin_amdgcn_s_memtime() - tl;
-      const uint64_t trav = ballot(tr.active);
-      const int ready = __popcll(ballot(!tr.active && has));
+      const uint64_t trav = ballot(trav_active(tr));
+      const int ready = __popcll(ballot(!trav_active(tr) && has));
       if (trav == 0 || ready >= need) break;
     }
     uint64_t t_shade0 = 0;
@@ -1064,9 +1071,9 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       t_shade0 = __builtin_amdgcn_s_memtime();
       w.diag[5] += t_shade0 - t_trav0;
       w.diag[3] += 1;
-      w.diag[4] += __popcll(ballot(!tr.active && has));
+      w.diag[4] += __popcll(ballot(!trav_active(tr) && has));
     }
-    if (!tr.active && has) {
+    if (!trav_active(tr) && has) {
       ++w.segs;
       bool alive_path;
       if (tr.best < 0) {
@@ -1258,7 +1265,7 @@ __global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCame
   while (sample < C.spp) {
     Trav tr;
     trav_begin(tr, S, ps.o, ps.d, ps.origin);
-    while (tr.active)
+    while (trav_active(tr))
       trav_step<LdsStack<STACK>, COUNT>(tr, S, ps.o, ps.d, ps.time, LdsStack<STACK>{stk}, cnt, overflow, corrupt);
     ++segs;
     bool alive;

@@ -32,12 +32,14 @@ namespace {
 constexpr int kMaxStackNeed = 4096;     // traversal stack entries per lane (LDS part + global spill)
 constexpr int kPlainWgsPerCu = 5;        // schedule 4 grid: resident workgroups per CU (waves pull work)
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
+constexpr int kTexShadeBatch = 56;      // ... and on scenes with image / noise textures
 constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
 // Scenes with a handful of BVH nodes once waited for 48 lanes (Cornell -15 % with the SAH cost 0.7
 // tree, profiles/r01_leafbatch); with the cost 0.5 tree and the ground occluder 12 is as good or
-// better there too (Cornell 13.97 -> 13.56 ms at 800x450x300, earth_perlin 17.40 vs 17.43 ms)
+// better there too (Cornell 13.97 -> 13.56 ms at 800x450x300, earth_perlin 17.40 vs 17.43 ms); with
+// the cheaper round-2 trip (kTravDone) 16 is best again: Cornell -1.2 %, earth_perlin +0.3 %
 constexpr int kSmallBvhNodes = 16;
-constexpr int kSmallBvhLeafBatch = 12;
+constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
 }
@@ -893,7 +895,10 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dj.row_stride = job->row_stride;
   dj.row_count = rows;
   const int batch = (job->flags >> 16) & 0xff;
-  dj.shade_batch = batch == 0 ? kDefaultShadeBatch : (batch > 64 ? 64 : batch);
+  // scenes with image / noise textures shade at a higher cost per lane: fuller shading batches
+  // (earth_perlin: 56 -2.2 % against 48; book-1 and Cornell keep 48, profiles/r02_ab)
+  const int default_shade = s->dev.tex_full ? kTexShadeBatch : kDefaultShadeBatch;
+  dj.shade_batch = batch == 0 ? default_shade : (batch > 64 ? 64 : batch);
   const int leaf_batch = (job->flags >> 24) & 0x7f;
   const int default_leaf_batch = s->dev.num_nodes <= kSmallBvhNodes ? kSmallBvhLeafBatch : kDefaultLeafBatch;
   dj.leaf_batch = leaf_batch == 0 ? default_leaf_batch : (leaf_batch > 64 ? 64 : leaf_batch);

@@ -368,7 +368,10 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
                                            bool& overflow, bool& corrupt) {
   constexpr bool PAIRS = GEOM != kGeomLds;
   // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
-  if (t.todo >= S.node_limit) {
+  // corrupt codes: checked wherever a bad code could fault (nodes through the vector-memory path)
+  // and in the COUNT diagnostics; an LDS read outside the allocation cannot fault, and the host
+  // validated the tree it copied there, so the hot LDS schedule skips the compare-and-branch
+  if ((GEOM != kGeomLds || COUNT) && t.todo >= S.node_limit) {
     corrupt = true;
     t.todo = kTravDone;
     return;
@@ -458,14 +461,15 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
-// Test the primitives of one leaf (t.todo < 0), then pop.
-template <class Stk, bool COUNT>
+// Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
+// LDS schedule outside the COUNT diagnostics, as for node codes).
+template <class Stk, bool COUNT, bool CHECK = true>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
   const int32_t code = ~t.todo;
   const int32_t first = code >> 3;
   const int32_t count = (code & 7) + 1;
-  if (static_cast<int64_t>(first) + count > S.num_refs) {
+  if ((CHECK || COUNT) && static_cast<int64_t>(first) + count > S.num_refs) {
     corrupt = true;
     t.todo = kTravDone;
     return;
@@ -952,8 +956,10 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   const int num_batches = J.num_tiles * J.chunks;
   V3 acc = v3(0.0f, 0.0f, 0.0f);
   uint32_t px = 0;
+  // s_end: end of the lane's unit (0: the lane holds no unit; an integer, not a bool, for the same
+  // reason as kTravDone: ballots of it need no lane-mask copy)
   int sample = 0, s_end = 0, chunk = 0;
-  bool has = false;
+  auto has = [&]() { return s_end != 0; };
   // fresh: the lane starts sample `sample` of its unit at the top of the next loop trip (the one
   // start path for the next sample of a unit and the first sample of a new unit); cont: its path
   // continues with a new segment (ps.o / ps.d scattered)
@@ -967,7 +973,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   for (;;) {
     // hand the next units of the current batch (new batches as needed) to the lanes without one
-    uint64_t want = ballot(!has);
+    uint64_t want = ballot(!has());
     while (want != 0 && !exhausted) {
       if (k_next >= 64) {
         int b = 0;
@@ -987,7 +993,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       const int take = min(__popcll(want), 64 - k_next);
       const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
           static_cast<uint32_t>(want >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(want), 0u)));
-      if (!has && rank < take) {
+      if (!has() && rank < take) {
         const int k = k_next + rank;
         const int i = bx + (k & ((1 << J.tile_lw) - 1));
         const int lr = by + (k >> J.tile_lw);
@@ -999,7 +1005,6 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
               o[0] = o[1] = o[2] = 0.0f;
             }
           } else {
-            has = true;
             fresh = true;
             chunk = bc;
             sample = bc * J.chunk_samples;
@@ -1009,7 +1014,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       k_next += take;
-      want = ballot(!has);
+      want = ballot(!has());
     }
     if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
     if (fresh || cont) {
@@ -1027,7 +1032,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     }
     fresh = false;
     cont = false;
-    const int alive = __popcll(ballot(has));
+    const uint64_t has_m = ballot(has());  // constant over the trip loop: kept as an SGPR mask
+    const int alive = __popcll(has_m);
     if (alive == 0) break;
     const int need = (alive * J.shade_batch + 63) >> 6;
     uint64_t t_trav0 = 0;
@@ -1036,7 +1042,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       if (COUNT) {
         w.diag[0] += 1;
         w.diag[1] += __popcll(ballot(trav_active(tr)));
-        w.diag[2] += __popcll(ballot(!has));
+        w.diag[2] += __popcll(ballot(!has()));
       }
       const int at_leaf = __popcll(ballot(tr.todo < 0));
       const bool inner_left = ballot(at_inner(tr)) != 0;
@@ -1052,7 +1058,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       if (leaf_trip && tr.todo < 0)
-        leaf_step<Stk, COUNT>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+        leaf_step<Stk, COUNT, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       if (at_inner(tr)) {
@@ -1063,7 +1069,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       }
       if (COUNT && leaf_trip) w.diag[8] += __builtin_amdgcn_s_memtime() - tl;
       const uint64_t trav = ballot(trav_active(tr));
-      const int ready = __popcll(ballot(!trav_active(tr) && has));
+      const int ready = __popcll(ballot(!trav_active(tr)) & has_m);
       if (trav == 0 || ready >= need) break;
     }
     uint64_t t_shade0 = 0;
@@ -1071,9 +1077,9 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       t_shade0 = __builtin_amdgcn_s_memtime();
       w.diag[5] += t_shade0 - t_trav0;
       w.diag[3] += 1;
-      w.diag[4] += __popcll(ballot(!trav_active(tr) && has));
+      w.diag[4] += __popcll(ballot(!trav_active(tr) && has()));
     }
-    if (!trav_active(tr) && has) {
+    if (!trav_active(tr) && has()) {
       ++w.segs;
       bool alive_path;
       if (tr.best < 0) {
@@ -1108,7 +1114,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
             o[1] = acc.y;
             o[2] = acc.z;
           }
-          has = false;
+          s_end = 0;  // the unit is done
           ++w.pixels;
         }
       }

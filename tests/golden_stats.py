@@ -72,13 +72,19 @@ def assert_statistical_parity(frame, m, n_frame, z_max=4.0, frac=0.999, global_s
     everywhere shows here first; the three channels of a block are strongly correlated, so the
     band counts blocks, not block-channels); the global mean of every channel within global_sigma
     standard errors. z_max covers the skew of block means at low sample counts (rare bright or
-    dark paths): 4 at GPU sample counts, 5 for the CPU oracle's few samples per pixel."""
+    dark paths): 4 at GPU sample counts, 5 for the CPU oracle's few samples per pixel.
+    At least two blocks may exceed z_max whatever the frame size: at 16 spp a light-lit scene's
+    block means are heavy-tailed, and across 40 seeds of the 120x120 Cornell frame (675
+    block-channels each) 9 block-channels exceeded 5 sigma with the PCG32 draws in use (4 with a
+    multiply-with-carry generator tried in round 2), so a "none of 675" rule (0.999 of 675) failed
+    about one seed in ten whatever the generator."""
     z, noisy, gz = block_z(frame, m["mean"], m["var"], n_frame, int(m["n"]))
     ok = float(np.mean(np.abs(z) < z_max))
+    outliers = int(np.sum(np.abs(z) >= z_max))
     zn = z[noisy]
     chi = float(np.mean(zn * zn))
     band = 6.0 * np.sqrt(2.0 * 3.0 / zn.size)  # 6 sigma of the chi-square mean, zn.size / 3 blocks
-    assert ok >= frac, (ok, float(np.abs(z).max()))
+    assert outliers <= max(2, int((1.0 - frac) * z.size)), (ok, outliers, float(np.abs(z).max()))
     assert abs(chi - 1.0) < band + 0.05, (chi, band)  # +0.05: non-gaussian tails of bright paths
     assert np.all(np.abs(gz) < global_sigma), gz.tolist()
     return {"blocks": int(z.size), "noisy": int(zn.size), "frac_ok": ok, "mean_z2": chi,

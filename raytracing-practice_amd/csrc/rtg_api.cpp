@@ -33,6 +33,7 @@ constexpr int kMaxStackNeed = 4096;     // traversal stack entries per lane (LDS
 constexpr int kPlainWgsPerCu = 5;        // schedule 4 grid: resident workgroups per CU (waves pull work)
 constexpr int kDefaultShadeBatch = 48;  // of 64 live lanes: measured best on book-1
 constexpr int kTexShadeBatch = 56;      // ... and on scenes with image / noise textures
+constexpr int kCacheShadeBatch = 40;    // ... and where nodes come through the caches (config 5)
 constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf trip
 // Scenes with a handful of BVH nodes once waited for 48 lanes (Cornell -15 % with the SAH cost 0.7
 // tree, profiles/r01_leafbatch); with the cost 0.5 tree and the ground occluder 12 is as good or
@@ -897,8 +898,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const int batch = (job->flags >> 16) & 0xff;
   // scenes with image / noise textures shade at a higher cost per lane: fuller shading batches
   // (earth_perlin: 56 -2.2 % against 48; book-1 and Cornell keep 48, profiles/r02_ab)
-  const int default_shade = s->dev.tex_full ? kTexShadeBatch : kDefaultShadeBatch;
-  dj.shade_batch = batch == 0 ? default_shade : (batch > 64 ? 64 : batch);
+  dj.shade_batch = batch > 64 ? 64 : batch;  // 0: the schedule's default, set below
   const int leaf_batch = (job->flags >> 24) & 0x7f;
   const int default_leaf_batch = s->dev.num_nodes <= kSmallBvhNodes ? kSmallBvhLeafBatch : kDefaultLeafBatch;
   dj.leaf_batch = leaf_batch == 0 ? default_leaf_batch : (leaf_batch > 64 ? 64 : leaf_batch);
@@ -955,6 +955,11 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     if (lds_bytes < 0) return fail(RTG_E_INVALID, "schedule 5: no LDS room for the treelet");
   }
   if (variant == 4) variant = 0;  // plain-grid ballot schedule
+  // shading batch: a trip costs more where node rows come through the caches (config 5: 40 -2.0 %
+  // against 48, profiles/r02_ab), shading more with image / noise textures (earth_perlin: 56 -2.2 %)
+  if (dj.shade_batch == 0)
+    dj.shade_batch = (variant == 5 || variant == 0) ? kCacheShadeBatch
+                                                    : (s->dev.tex_full ? kTexShadeBatch : kDefaultShadeBatch);
   if (variant == 3 && lds_bytes < 0) return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
   if ((variant == 1 || variant == 2) && s->dev.node_width != 2)
     return fail(RTG_E_INVALID, "schedules 1 and 2 need a binary BVH (RTG_BVH_MEDIAN)");

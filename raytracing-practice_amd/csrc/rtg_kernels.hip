@@ -1061,11 +1061,18 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         leaf_step<Stk, COUNT, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
-      if (at_inner(tr)) {
-        if constexpr (WIDE == 4)
-          node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
-        else
-          node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+      // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
+      // overhead, and a lane's second step overlaps the other lanes' load latency), 1 for LDS scenes
+      // (2: neutral, 3: +3 %)
+      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : 2;
+#pragma unroll
+      for (int rep = 0; rep < kNodeReps; ++rep) {
+        if (at_inner(tr)) {
+          if constexpr (WIDE == 4)
+            node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+          else
+            node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+        }
       }
       if (COUNT && leaf_trip) w.diag[8] += __builtin_amdgcn_s_memtime() - tl;
       const uint64_t trav = ballot(trav_active(tr));

@@ -154,8 +154,9 @@ def cpu_baseline(args, scene_desc, cam):
 
 
 def pmc_traffic(workload):
-    """HBM bytes per render launch measured by rocprofv3 PMC passes (profiles/pmc_*.json, written by
-    profiles/collect_pmc.py for the same workload); None when no matching measurement exists."""
+    """HBM bytes per render launch measured by rocprofv3 PMC passes (profiles/pmc_traffic.json,
+    written by tools/pmc_report.py --write-traffic from tools/profile.sh passes of the same workload);
+    None when no matching measurement exists."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:

@@ -617,6 +617,15 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
   const float uu = u * u * (3.0f - 2.0f * u);
   const float vv = v * v * (3.0f - 2.0f * v);
   const float ww = w * w * (3.0f - 2.0f * w);
+  // the six permutation entries, then all eight corner gradients, are fetched before any of them is
+  // used: one LDS round trip each instead of eight dependent ones per octave (config 3 shades 7
+  // octaves per ground hit); the sum below keeps the reference's corner order
+  const int px[2] = {perm[i & 255], perm[(i + 1) & 255]};
+  const int py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
+  const int pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
+  float4 g[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) g[c] = vec[px[c >> 2] ^ py[(c >> 1) & 1] ^ pz[c & 1]];
   float accum = 0.0f;
 #pragma unroll
   for (int di = 0; di < 2; ++di) {
@@ -624,9 +633,7 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
     for (int dj = 0; dj < 2; ++dj) {
 #pragma unroll
       for (int dk = 0; dk < 2; ++dk) {
-        const int idx = perm[(i + di) & 255] ^ perm[256 + ((j + dj) & 255)] ^
-                        perm[512 + ((k + dk) & 255)];
-        const V3 c = xyz(vec[idx]);
+        const V3 c = xyz(g[di * 4 + dj * 2 + dk]);
         const V3 wv = v3(u - di, v - dj, w - dk);
         const float fu = di ? uu : (1.0f - uu);
         const float fv = dj ? vv : (1.0f - vv);
@@ -972,6 +979,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   tr.todo = kTravDone;
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   for (;;) {
+    uint64_t t_top = 0;
+    if (COUNT) t_top = __builtin_amdgcn_s_memtime();
     // hand the next units of the current batch (new batches as needed) to the lanes without one
     uint64_t want = ballot(!has());
     while (want != 0 && !exhausted) {
@@ -1016,7 +1025,15 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       k_next += take;
       want = ballot(!has());
     }
+    uint64_t t_start = 0;
+    if (COUNT) t_start = __builtin_amdgcn_s_memtime();
     if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
+    if (COUNT) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      w.diag[13] += t_start - t_top;  // unit hand-out
+      w.diag[14] += t - t_start;      // camera rays of fresh samples
+      t_start = t;
+    }
     if (fresh || cont) {
       trav_begin(tr, S, ps.o, ps.d, ps.origin);
       if (S.occluder >= 0) {  // the scene-spanning sphere kept out of the BVH (DevScene::occluder)
@@ -1032,6 +1049,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     }
     fresh = false;
     cont = false;
+    if (COUNT) w.diag[15] += __builtin_amdgcn_s_memtime() - t_start;  // trav_begin + occluder test
     const uint64_t has_m = ballot(has());  // constant over the trip loop: kept as an SGPR mask
     const int alive = __popcll(has_m);
     if (alive == 0) break;

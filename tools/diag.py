@@ -56,7 +56,11 @@ def main():
                   "leaf_trip_lane_util": d[10] / (64 * max(1, d[7])),
                   "node_steps_per_segment": d[9] / st.segments,
                   "leaf_steps_per_segment": d[10] / st.segments,
-                  "shade_split_scatter_end_setup": [round(d[k] / max(1, d[6]), 3) for k in (11, 12, 13)]}
+                  "shade_split_scatter_end": [round(d[k] / max(1, d[6]), 3) for k in (11, 12)],
+                  # wave cycles of the whole loop: traversal, shading, and the restart between them
+                  # (unit hand-out, camera rays of fresh samples, trav_begin + occluder test)
+                  "cycle_split_trav_shade_handout_camera_begin": [
+                      round(d[k] / max(1, d[5] + d[6] + d[13] + d[14] + d[15]), 3) for k in (5, 6, 13, 14, 15)]}
     print(json.dumps(out, indent=1))
 
 

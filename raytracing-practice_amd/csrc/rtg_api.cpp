@@ -42,6 +42,7 @@ constexpr int kDefaultLeafBatch = 12;   // lanes waiting at a leaf before a leaf
 constexpr int kSmallBvhNodes = 16;
 constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
+constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
 constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
 }
 
@@ -945,7 +946,25 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   DevScene dscene = s->dev;  // this render's view (the treelet schedule sets its LDS part)
   dj.lds_sphere_f4 = 3;      // 48-B sphere records in LDS (bank spread)
   if (const char* e = std::getenv("RTG_LDS_SPHERE_F4")) dj.lds_sphere_f4 = std::atoi(e) == 2 ? 2 : 3;  // A/B
+  // persistent LDS schedule: one 16-wave workgroup per CU (4 waves per SIMD, the most one workgroup
+  // can hold), or, for scenes small enough that five copies of scene + stacks fit one CU's LDS, five
+  // 4-wave workgroups per CU: 5 waves per SIMD at <= 96 VGPRs (Cornell -9.3 %, earth_perlin -0.7 %;
+  // book-1's 78 KB scene does not fit twice). RTG_LDS_WAVES=16 keeps the single workgroup (A/B).
+  dj.lds_waves = kLdsWaves;
   int lds_bytes = lds_layout(dscene, kLdsStack, kLdsWaves, &dj);
+  int lds_wgs = 1;  // persistent workgroups per CU
+  {
+    const char* e = std::getenv("RTG_LDS_WAVES");
+    DevJob t = dj;
+    const int b4 = lds_layout(dscene, kLdsStack, 4, &t);
+    if ((!e || std::atoi(e) == 4) && dscene.node_width == 4 && !std::getenv("RTG_STACK_LDS_ENTRIES") &&
+        need <= kLdsStack && b4 > 0 && b4 * kSmallSceneWgs <= 160 * 1024) {
+      dj = t;
+      dj.lds_waves = 4;
+      lds_bytes = b4;
+      lds_wgs = kSmallSceneWgs;
+    }
+  }
   // default: the whole scene in LDS (3); else the top of a 4-wide tree in LDS (5, config 5's 1M
   // spheres: -1.3 % against 4, profiles/r02_ab), else the plain grid (4)
   if (variant == 0) variant = lds_bytes > 0 ? 3 : (dscene.node_width == 4 ? 5 : 4);
@@ -967,8 +986,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   int grid_blocks = 1, grid_waves = 0;
   if (variant == 3 || variant == 5) {
     stack_depth = kLdsStack;
-    grid_blocks = std::max(1, std::min(s->num_cus, dj.num_tiles));
-    grid_waves = grid_blocks * kLdsWaves;
+    grid_blocks = std::max(1, std::min(s->num_cus * (variant == 3 ? lds_wgs : 1), dj.num_tiles));
+    grid_waves = grid_blocks * (variant == 3 ? dj.lds_waves : kLdsWaves);
   } else if (variant == 0) {
     stack_depth = need <= 16 ? 16 : 32;
     grid_blocks = std::max(1, std::min(s->num_cus * kPlainWgsPerCu, (dj.num_tiles + 3) / 4));

@@ -189,6 +189,7 @@ struct DevJob {
   int32_t lds_nodes, lds_refs, lds_spheres, lds_quads, lds_materials, lds_textures;
   int32_t lds_perlin_vec, lds_perlin_perm;  // noise tables (full-texture kernels only)
   int32_t lds_sphere_f4;                     // float4s per sphere record in the LDS copy (2 or 3)
+  int32_t lds_waves;                         // persistent LDS kernel: waves per workgroup
 
 };
 

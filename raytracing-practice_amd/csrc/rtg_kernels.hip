@@ -1182,7 +1182,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
 // through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
 template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM>
-__global__ __launch_bounds__(WAVES * 64) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
+__global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
@@ -1415,19 +1415,19 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
-template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds>
+template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int WAVES = kLdsWaves>
 hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
                       int lds_bytes, int grid_blocks, hipStream_t stream) {
-  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF, GEOM>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF, GEOM>);
+  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (count)
-    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, kLdsWaves, WIDE, TEXF, GEOM>), dim3(grid_blocks),
-                       dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>), dim3(grid_blocks),
+                       dim3(WAVES * 64), lds_bytes, stream, S, C, J);
   else
-    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, kLdsWaves, WIDE, TEXF, GEOM>), dim3(grid_blocks),
-                       dim3(kLdsWaves * 64), lds_bytes, stream, S, C, J);
+    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>), dim3(grid_blocks),
+                       dim3(WAVES * 64), lds_bytes, stream, S, C, J);
   return hipGetLastError();
 }
 
@@ -1467,6 +1467,9 @@ hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J
     if (spill)
       return tex ? launch_lds<kLdsStack, true, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
                  : launch_lds<kLdsStack, true, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+    if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU (A/B)
+      return tex ? launch_lds<kLdsStack, false, WIDE, true, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream)
+                 : launch_lds<kLdsStack, false, WIDE, false, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream);
     return tex ? launch_lds<kLdsStack, false, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
                : launch_lds<kLdsStack, false, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
   }

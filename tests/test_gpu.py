@@ -161,6 +161,26 @@ def test_schedules_give_identical_frames(gpu_lib, scenes):
     assert max(segs) - min(segs) <= 2
 
 
+@pytest.mark.parametrize("name,W,spp,depth", [("cornell_box", 96, 16, 100), ("earth_perlin", 128, 8, 50)])
+def test_small_scene_workgroup_shapes(gpu_lib, scenes, oracle, name, W, spp, depth, monkeypatch):
+    """Scenes small enough for five copies of scene + stacks per CU run five 4-wave persistent
+    workgroups per CU (5 waves per SIMD) instead of one 16-wave one: the work units are the same,
+    so the frame and the segment count are identical, and both match the oracle."""
+    s = scenes.build(name, rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = W, spp, depth
+    out = {}
+    for waves in ("4", "16"):
+        monkeypatch.setenv("RTG_LDS_WAVES", waves)
+        ds = gpu_lib.scene_create(s.desc)
+        out[waves] = ds.render_host(c)
+        ds.close()
+    (g4, st4), (g16, st16) = out["4"], out["16"]
+    assert np.array_equal(g4, g16) and st4.segments == st16.segments
+    o, segs = oracle.render_f32(s.desc, c)
+    assert np.sqrt(np.mean((g4.astype(np.float64) - o) ** 2)) < 1e-3
+
+
 @pytest.mark.parametrize("grid,W", [(11, 96), (500, 128)])
 def test_treelet_schedule_matches_default(gpu_lib, scenes, oracle, grid, W, monkeypatch):
     """Schedule 5 (persistent workgroups, the breadth-first top of the 4-wide tree in LDS, the rest

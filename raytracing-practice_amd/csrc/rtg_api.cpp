@@ -5,6 +5,7 @@
 // the gfx950 render kernel (rtg_kernels.hip) on the caller's stream. No CPU fallback exists:
 // without a usable device every entry point that renders returns RTG_E_NODEVICE / RTG_E_HIP.
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -21,7 +22,7 @@ hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, in
                           hipStream_t stream);
 hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
                          bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream);
-int lds_layout(const DevScene& S, int stack, int waves, DevJob* J);
+int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J);
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J);
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
 }  // namespace rtg
@@ -460,19 +461,41 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     f[15] = 0.0f;
   }
 
-  // materials {type, texture, fuzz, eta}, {albedo.xyz, uses_uv}
+  // materials {type, texture, fuzz, eta}, {albedo.xyz, uses_uv}. A lambertian or diffuse_light whose
+  // texture is a solid_color carries the colour itself (texture -1, albedo = the colour: the value
+  // solid_color::value returns, texture.hpp:34-44), and only the textures some material still
+  // references (checkers and their children, images, noise) are kept, renumbered: book-1's 388
+  // per-sphere solid textures (12.4 KB of LDS) disappear and its shading skips a dependent fetch.
+  auto is_textured = [&](const rtg_material& mt) {
+    return mt.type == RTG_MAT_LAMBERTIAN || mt.type == RTG_MAT_DIFFUSE_LIGHT;
+  };
+  std::vector<int32_t> tex_map(static_cast<size_t>(d->num_textures), -1);
+  std::vector<int32_t> tex_order;
+  std::function<void(int32_t)> keep = [&](int32_t t) {
+    if (t < 0 || t >= d->num_textures || tex_map[t] >= 0) return;
+    tex_map[t] = static_cast<int32_t>(tex_order.size());
+    tex_order.push_back(t);
+    if (d->textures[t].type == RTG_TEX_CHECKER) {
+      keep(d->textures[t].even);
+      keep(d->textures[t].odd);
+    }
+  };
+  for (int32_t m = 0; m < d->num_materials; ++m)
+    if (is_textured(d->materials[m]) && d->textures[d->materials[m].texture].type != RTG_TEX_SOLID)
+      keep(d->materials[m].texture);
   for (int32_t m = 0; m < d->num_materials; ++m) {
     const rtg_material& mt = d->materials[m];
     const double fuzz = mt.fuzz < 1.0f ? mt.fuzz : 1.0f;  // metal ctor clamp (material.hpp:83)
-    const bool uv = (mt.type == RTG_MAT_LAMBERTIAN || mt.type == RTG_MAT_DIFFUSE_LIGHT) &&
-                    texture_uses_uv(d, mt.texture, 0);
+    const bool uv = is_textured(mt) && texture_uses_uv(d, mt.texture, 0);
+    const bool inline_solid = is_textured(mt) && d->textures[mt.texture].type == RTG_TEX_SOLID;
+    const double* alb = inline_solid ? d->textures[mt.texture].color : mt.albedo;
     const float rec[8] = {ibits_to_float(mt.type),
-                          ibits_to_float(mt.texture),
+                          ibits_to_float(inline_solid ? -1 : (is_textured(mt) ? tex_map[mt.texture] : -1)),
                           static_cast<float>(fuzz),
                           static_cast<float>(mt.refraction_index),
-                          static_cast<float>(mt.albedo[0]),
-                          static_cast<float>(mt.albedo[1]),
-                          static_cast<float>(mt.albedo[2]),
+                          static_cast<float>(alb[0]),
+                          static_cast<float>(alb[1]),
+                          static_cast<float>(alb[2]),
                           ibits_to_float(uv ? 1 : 0)};
     out->materials.insert(out->materials.end(), rec, rec + 8);
   }
@@ -495,7 +518,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       }
     }
   }
-  for (int32_t t = 0; t < d->num_textures; ++t) {
+  for (const int32_t t : tex_order) {
     const rtg_texture& tx = d->textures[t];
     float scale = 0.0f;
     int32_t aux = -1;
@@ -505,9 +528,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       aux = tx.perlin;
     }
     if (tx.type == RTG_TEX_IMAGE) aux = (tx.image >= 0 && tx.image < d->num_images) ? tx.image : -1;
+    const bool checker = tx.type == RTG_TEX_CHECKER;
     const float rec[8] = {ibits_to_float(tx.type),
-                          ibits_to_float(tx.even),
-                          ibits_to_float(tx.odd),
+                          ibits_to_float(checker ? tex_map[tx.even] : tx.even),
+                          ibits_to_float(checker ? tex_map[tx.odd] : tx.odd),
                           scale,
                           static_cast<float>(tx.color[0]),
                           static_cast<float>(tx.color[1]),
@@ -542,6 +566,8 @@ struct rtg_scene {
   int device = 0;
   int num_cus = 0;
   hipStream_t own_stream = nullptr;
+  hipStream_t aux_stream = nullptr;  // second persistent launch (dual workgroup shapes)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   void* dmem = nullptr;  // one allocation for all scene arrays
   size_t dbytes = 0;
@@ -804,6 +830,9 @@ void rtg_scene_destroy(rtg_scene* s) {
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
+  if (s->aux_stream) (void)hipStreamDestroy(s->aux_stream);
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   delete s;
 }
 
@@ -945,24 +974,56 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const int need = std::max(1, s->stack_need);
   DevScene dscene = s->dev;  // this render's view (the treelet schedule sets its LDS part)
   dj.lds_sphere_f4 = 3;      // 48-B sphere records in LDS (bank spread)
-  if (const char* e = std::getenv("RTG_LDS_SPHERE_F4")) dj.lds_sphere_f4 = std::atoi(e) == 2 ? 2 : 3;  // A/B
-  // persistent LDS schedule: one 16-wave workgroup per CU (4 waves per SIMD, the most one workgroup
-  // can hold), or, for scenes small enough that five copies of scene + stacks fit one CU's LDS, five
-  // 4-wave workgroups per CU: 5 waves per SIMD at <= 96 VGPRs (Cornell -9.3 %, earth_perlin -0.7 %;
-  // book-1's 78 KB scene does not fit twice). RTG_LDS_WAVES=16 keeps the single workgroup (A/B).
+  // persistent LDS schedule, by scene size (DESIGN.md §3 "occupancy"): five 4-wave workgroups per CU
+  // when five copies of scene + stacks fit one CU's LDS (5 waves per SIMD at <= 96 VGPRs; Cornell
+  // -9.3 %); else one 16-wave workgroup (4 waves per SIMD, the most one workgroup holds) plus, when a
+  // second copy fits beside it, a 4-wave workgroup from a second persistent launch (dual, below); else
+  // the 16-wave workgroup alone. RTG_LDS_WAVES=16 keeps the single workgroup, RTG_DUAL=0 no dual.
+  // stack entries of the persistent LDS schedule: 16-bit for 4-wide trees whose leaf codes fit 16 bits
+  // and whose stack needs no spill (kernel LdsStack16), else 32-bit
+  const char* lds_entries_env = std::getenv("RTG_STACK_LDS_ENTRIES");
+  const bool stk16 = dscene.node_width == 4 && dscene.num_refs <= 4096 && need <= kLdsStack && !lds_entries_env &&
+                     !dscene.tex_full;
+  dj.stack_esz = stk16 ? 2 : 4;
   dj.lds_waves = kLdsWaves;
-  int lds_bytes = lds_layout(dscene, kLdsStack, kLdsWaves, &dj);
+  int lds_bytes = lds_layout(dscene, kLdsStack, kLdsWaves, dj.stack_esz, &dj);
   int lds_wgs = 1;  // persistent workgroups per CU
   {
     const char* e = std::getenv("RTG_LDS_WAVES");
     DevJob t = dj;
-    const int b4 = lds_layout(dscene, kLdsStack, 4, &t);
-    if ((!e || std::atoi(e) == 4) && dscene.node_width == 4 && !std::getenv("RTG_STACK_LDS_ENTRIES") &&
-        need <= kLdsStack && b4 > 0 && b4 * kSmallSceneWgs <= 160 * 1024) {
+    const int b4 = lds_layout(dscene, kLdsStack, 4, dj.stack_esz, &t);
+    if ((!e || std::atoi(e) == 4) && dscene.node_width == 4 && need <= kLdsStack && !lds_entries_env && b4 > 0 &&
+        b4 * kSmallSceneWgs <= 160 * 1024 && (stk16 || dscene.tex_full)) {
       dj = t;
       dj.lds_waves = 4;
       lds_bytes = b4;
       lds_wgs = kSmallSceneWgs;
+    }
+  }
+  // dual: the 16-wave workgroup's kernel (<= 104 VGPRs, tex_full off) leaves 96 registers per SIMD
+  // lane (4 x 104 + 96 = 512) for one wave of the 4-wave kernel (<= 96 VGPRs); LDS must hold both
+  // copies, with 32-B sphere records if the padded 48-B ones do not fit (book-1: 90 + 66 KB)
+  DevJob j4{};
+  int lds4 = -1;
+  {
+    const char* e = std::getenv("RTG_DUAL");
+    const char* ew = std::getenv("RTG_LDS_WAVES");
+    if (dj.lds_waves == kLdsWaves && stk16 && !dscene.tex_full && !(e && std::atoi(e) == 0) &&
+        !(ew && std::atoi(ew) == 16)) {
+      for (const int f4 : {3, 2}) {
+        DevJob a = dj, b = dj;
+        a.lds_sphere_f4 = b.lds_sphere_f4 = f4;
+        const int b16 = lds_layout(dscene, kLdsStack, kLdsWaves, 2, &a);
+        const int bb4 = lds_layout(dscene, kLdsStack, 4, 2, &b);
+        if (b16 > 0 && bb4 > 0 && b16 + bb4 <= 160 * 1024) {
+          dj = a;
+          lds_bytes = b16;
+          j4 = b;
+          j4.lds_waves = 4;
+          lds4 = bb4;
+          break;
+        }
+      }
     }
   }
   // default: the whole scene in LDS (3); else the top of a 4-wide tree in LDS (5, config 5's 1M
@@ -970,6 +1031,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (variant == 0) variant = lds_bytes > 0 ? 3 : (dscene.node_width == 4 ? 5 : 4);
   if (variant == 5) {  // persistent workgroups with the top of the tree in LDS (4-wide trees)
     if (dscene.node_width != 4) return fail(RTG_E_INVALID, "schedule 5 needs a 4-wide BVH (RTG_BVH_SAH)");
+    dj.stack_esz = 4;
+    dj.lds_waves = kLdsWaves;
     lds_bytes = lds_layout_treelet(&dscene, kLdsStack, kLdsWaves, &dj);
     if (lds_bytes < 0) return fail(RTG_E_INVALID, "schedule 5: no LDS room for the treelet");
   }
@@ -999,7 +1062,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (const char* e = std::getenv("RTG_STACK")) stack_depth = std::atoi(e);  // experiments only
   dj.lds_stack = stack_depth;
   // RTG_STACK_LDS_ENTRIES (tests): keep fewer entries in LDS so the global spill path is exercised
-  if (const char* e = std::getenv("RTG_STACK_LDS_ENTRIES"))
+  if (const char* e = lds_entries_env)
     dj.lds_stack = std::min(stack_depth, std::max(1, std::atoi(e)));
   const bool default_sched = variant == 3 || variant == 0 || variant == 5;  // the ballot-batched stream
   dj.spill_depth = default_sched ? std::max(0, need - dj.lds_stack) : 0;
@@ -1040,10 +1103,34 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
                            out_bytes * dj.chunks, stream),
             "hipMemsetAsync(partial sums)");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
+  if (skip_kernel || variant != 3) lds4 = -1;
+  if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
+    const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
+                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm};
+    j4 = dj;
+    j4.lds_waves = 4;
+    j4.lds_nodes = l4[0], j4.lds_refs = l4[1], j4.lds_spheres = l4[2], j4.lds_quads = l4[3];
+    j4.lds_materials = l4[4], j4.lds_textures = l4[5], j4.lds_perlin_vec = l4[6], j4.lds_perlin_perm = l4[7];
+    j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
+  }
+  if (lds4 > 0) {
+    if (!s->aux_stream) RTG_HIP(hipStreamCreateWithFlags(&s->aux_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!s->ev_fork) RTG_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    if (!s->ev_join) RTG_HIP(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming), "hipEventCreate");
+    RTG_HIP(hipEventRecord(s->ev_fork, stream), "hipEventRecord");
+    RTG_HIP(hipStreamWaitEvent(s->aux_stream, s->ev_fork, 0), "hipStreamWaitEvent");
+  }
   if (!skip_kernel)
     RTG_HIP(launch_render(dscene, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
                           variant, lds_bytes, grid_blocks, stream),
             "render kernel launch");
+  if (lds4 > 0) {
+    RTG_HIP(launch_render(dscene, dc, j4, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0, variant, lds4,
+                          s->num_cus, s->aux_stream),
+            "render kernel launch (aux)");
+    RTG_HIP(hipEventRecord(s->ev_join, s->aux_stream), "hipEventRecord");
+    RTG_HIP(hipStreamWaitEvent(stream, s->ev_join, 0), "hipStreamWaitEvent");
+  }
   if (chunked || (progressive && dout))
     RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, sum_chunks, out_scale, stream),
             "combine kernel launch");

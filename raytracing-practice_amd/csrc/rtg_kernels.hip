@@ -231,6 +231,17 @@ struct LdsStack {
   __device__ __forceinline__ void store(int32_t sp, int32_t v) const { lds[sp * 64] = v; }
   __device__ __forceinline__ int32_t load(int32_t sp) const { return lds[sp * 64]; }
 };
+// LdsStack16: 16-bit entries for the LDS schedule of 4-wide trees (inner-node codes are LDS byte
+// addresses / 16 < 10240, leaf codes ~((first << 3) | (count - 1)) with first < 4096 — the host
+// checks): half the LDS of 32-bit entries, which is what lets a second persistent launch share the
+// CU with book-1 (DESIGN.md §3 "occupancy").
+template <int N>
+struct LdsStack16 {
+  int16_t* lds;
+  __device__ __forceinline__ int32_t capacity() const { return N; }
+  __device__ __forceinline__ void store(int32_t sp, int32_t v) const { lds[sp * 64] = static_cast<int16_t>(v); }
+  __device__ __forceinline__ int32_t load(int32_t sp) const { return lds[sp * 64]; }
+};
 template <int N>
 struct SpillStack {
   int32_t* lds;
@@ -378,7 +389,8 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
   const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
-  const uint32_t na = static_cast<uint32_t>(t.todo);  // LDS scenes: the node's LDS address
+  // LDS scenes: inner-node codes are the node's LDS byte address / 16 (nodes are 16-byte aligned)
+  const uint32_t na = GEOM == kGeomLds ? static_cast<uint32_t>(t.todo) << 4 : static_cast<uint32_t>(t.todo);
   nf4 nx, ny, nz, fx, fy, fz;
   int4 cc;
   if constexpr (GEOM == kGeomLds) {
@@ -792,7 +804,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
 
   if (type == RTG_MAT_DIFFUSE_LIGHT) {
     if (needs_uv) sphere_uv();
-    const V3 e = texture_value<FULL>(S, tex, u, v, p);
+    const V3 e = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);  // < 0: solid colour inline
     ps.L = add(ps.L, mul(ps.T, e));
     return false;
   }
@@ -806,7 +818,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
       const float s = 1e-8f;
       if (fabsf(dir.x) < s && dir.y < s && fabsf(dir.z) < s) dir = n;
       if (needs_uv) sphere_uv();
-      att = texture_value<FULL>(S, tex, u, v, p);
+      att = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);
     } else {
       const V3 in = ps.d;
       const V3 refl = sub(in, scl(2.0f * dot(in, n), n));
@@ -1184,10 +1196,15 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM>
 __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // the whole-scene LDS schedule of 4-wide trees without a stack spill and without image / noise
+  // textures keeps 16-bit stack entries (the LDS room that lets book-1 run the dual launch; the
+  // textured kernels keep 32-bit ones: earth_perlin +2 % with 16-bit)
+  constexpr bool STK16 = GEOM == kGeomLds && WIDE == 4 && !SPILL && !TEXF;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   int32_t* lstk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
+  int16_t* lstk16 = reinterpret_cast<int16_t*>(smem) + wave * STACK * 64 + lane;
   if constexpr (GEOM == kGeomTreelet) {
     float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
     for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += WAVES * 64) l_top[k] = S.nodes[k];
@@ -1222,12 +1239,12 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) unsigned char*)smem))) + J.lds_nodes;
   for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) {
     float4 v = S.nodes[k];
-    if (WIDE == 4 && k % 7 == 6) {  // code row: inner-node codes become absolute LDS addresses
+    if (WIDE == 4 && k % 7 == 6) {  // code row: inner-node codes become absolute LDS addresses / 16
       int4 c = *reinterpret_cast<int4*>(&v);
-      c.x = c.x >= 0 ? c.x + node_rebase : c.x;
-      c.y = c.y >= 0 ? c.y + node_rebase : c.y;
-      c.z = c.z >= 0 ? c.z + node_rebase : c.z;
-      c.w = c.w >= 0 ? c.w + node_rebase : c.w;
+      c.x = c.x >= 0 ? (c.x + node_rebase) >> 4 : c.x;
+      c.y = c.y >= 0 ? (c.y + node_rebase) >> 4 : c.y;
+      c.z = c.z >= 0 ? (c.z + node_rebase) >> 4 : c.z;
+      c.w = c.w >= 0 ? (c.w + node_rebase) >> 4 : c.w;
       v = *reinterpret_cast<float4*>(&c);
     }
     l_nodes[k] = v;
@@ -1248,9 +1265,9 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
-  if (WIDE == 4) {  // inner-node codes are absolute LDS byte addresses
-    L.root_code = node_rebase;
-    L.node_limit = node_rebase + static_cast<int32_t>(S.num_nodes) * 112;
+  if (WIDE == 4) {  // inner-node codes are absolute LDS byte addresses / 16
+    L.root_code = node_rebase >> 4;
+    L.node_limit = (node_rebase + static_cast<int32_t>(S.num_nodes) * 112) >> 4;
   }
   L.refs = l_refs;
   L.spheres = l_spheres;
@@ -1268,6 +1285,8 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
     render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, stk, w);
+  } else if constexpr (STK16) {
+    render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, LdsStack16<STACK>{lstk16}, w);
   } else {
     render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, LdsStack<STACK>{lstk}, w);
   }
@@ -1434,7 +1453,8 @@ hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bo
 // Schedule 5: the persistent kernel with an LDS treelet over a scene in HBM (4-wide trees only).
 hipError_t launch_treelet(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int lds_bytes,
                           int grid_blocks, hipStream_t stream) {
-  if (S.node_width != 4 || J.lds_stack > kLdsStack) return hipErrorInvalidValue;
+  if (S.node_width != 4 || J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves)
+    return hipErrorInvalidValue;
   const bool spill = J.spill_depth > 0, tex = S.tex_full != 0;
   if (spill)
     return tex ? launch_lds<kLdsStack, true, 4, true, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream)
@@ -1464,7 +1484,12 @@ hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J
   const bool tex = S.tex_full != 0;
   if (lds) {
     if (stack != kLdsStack || J.lds_stack > kLdsStack) return hipErrorInvalidValue;
-    if (spill)
+    // 4-wide trees keep 16-bit stack entries (J.stack_esz 2) unless their leaf codes do not fit 16
+    // bits (the host then asks for 4-byte entries, which the spill variant holds, with no spill area
+    // if none is needed); binary trees keep 32-bit entries
+    const bool stk16 = WIDE == 4 && !spill && !tex && J.stack_esz == 2;
+    if (J.stack_esz != (stk16 ? 2 : 4)) return hipErrorInvalidValue;
+    if (spill || (WIDE == 4 && !tex && !stk16))
       return tex ? launch_lds<kLdsStack, true, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
                  : launch_lds<kLdsStack, true, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU (A/B)
@@ -1514,9 +1539,9 @@ int kernel_stack_depth(int bvh_depth) {
 
 // Dynamic LDS bytes of the persistent kernel for this scene, or -1 when it does not fit in
 // one CU's 160 KiB; fills the scene-copy offsets of the job.
-int lds_layout(const DevScene& S, int stack, int waves, DevJob* J) {
+int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   auto a16 = [](int64_t x) { return (x + 15) & ~int64_t(15); };
-  int64_t off = int64_t(waves) * stack * 64 * 4;  // traversal stacks
+  int64_t off = a16(int64_t(waves) * stack * 64 * esz);  // traversal stacks (esz bytes per entry)
   const int64_t nodes = off;
   off = a16(off + S.num_nodes * (S.node_width == 4 ? 112 : 64));
   const int64_t spheres = off;

@@ -181,6 +181,36 @@ def test_small_scene_workgroup_shapes(gpu_lib, scenes, oracle, name, W, spp, dep
     assert np.sqrt(np.mean((g4.astype(np.float64) - o) ** 2)) < 1e-3
 
 
+def test_dual_launch_matches_single(gpu_lib, scenes, monkeypatch):
+    """Book-1 is too large for five 4-wave workgroups per CU, so a second persistent launch (one
+    4-wave workgroup per CU on an auxiliary stream, beside the 16-wave one) fills the fifth wave slot
+    of each SIMD; both launches take units from one counter, so the frame and the segment count are
+    those of the single launch (RTG_DUAL=0) and of the plain grid."""
+    import ctypes as C
+
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 240, 24, 50  # 24 spp: two sample chunks
+    out = {}
+    for dual in ("1", "0"):
+        monkeypatch.setenv("RTG_DUAL", dual)
+        ds = gpu_lib.scene_create(s.desc)
+        out[dual] = ds.render_host(c)
+        ds.close()
+    monkeypatch.delenv("RTG_DUAL")
+    ds = gpu_lib.scene_create(s.desc)
+    H = gpu_lib.camera_resolve(c).image_height
+    ref = np.zeros((H, 240, 3), dtype=np.float32)
+    rst = rtgpu.rtg_render_stats()
+    job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, 0, 1, 0, rtgpu.RTG_RENDER_SCHEDULE(4), None)
+    gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job),
+                                                        ref.ctypes.data, C.byref(rst)))
+    ds.close()
+    (g1, st1), (g0, st0) = out["1"], out["0"]
+    assert np.array_equal(g1, g0) and st1.segments == st0.segments
+    assert np.array_equal(g1, ref) and st1.segments == rst.segments
+
+
 @pytest.mark.parametrize("grid,W", [(11, 96), (500, 128)])
 def test_treelet_schedule_matches_default(gpu_lib, scenes, oracle, grid, W, monkeypatch):
     """Schedule 5 (persistent workgroups, the breadth-first top of the 4-wide tree in LDS, the rest

@@ -156,7 +156,9 @@ typedef struct rtg_camera_params {
 /* Diagnostic schedule selection (A/B of kernel variants; 0 = the default everywhere):
  * bits 8-15 schedule (0 default = 3 when the scene geometry fits in LDS, else 5 for 4-wide trees,
  * else 4; 1 one closest-hit query per loop trip; 2 the first kernel (1 and 2 need a binary BVH:
- * RTG_BVH_MEDIAN); 3 persistent 16-wave workgroups with LDS-resident geometry; 4 ballot-batched on
+ * RTG_BVH_MEDIAN); 3 persistent workgroups with LDS-resident geometry (five 4-wave workgroups per
+ * CU for small scenes, else a 16-wave one plus, where it fits, a second launch of one 4-wave
+ * workgroup per CU: 5 waves per SIMD); 4 ballot-batched on
  * a plain grid, scene through the caches; 5 the persistent workgroups with the breadth-first top
  * of a 4-wide tree in LDS and the rest through the caches),
  * bits 16-23 shade batch of schedule 0 in 64ths of the live lanes (0 = library default). */
@@ -215,8 +217,9 @@ typedef struct rtg_render_stats {
    * [7] traversal trips that were leaf trips, [8] shader-clock cycles of the leaf trips,
    * [9] lanes that ran a node step summed over node trips, [10] lanes that ran a leaf step summed
    * over leaf trips; cycles of the shading phase split into [11] miss / material scatter,
-   * [12] path end (sample restart or chunk store), [13] traversal setup of the next segment;
-   * [14], [15] reserved */
+   * [12] path end (sample restart or chunk store); cycles between shading and the next traversal:
+   * [13] unit hand-out, [14] camera rays of fresh samples, [15] traversal setup (trav_begin and
+   * the scene-spanning occluder test) */
   uint64_t diag[16];
 } rtg_render_stats;
 

@@ -24,6 +24,7 @@ hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J,
                          bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream);
 int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J);
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J);
+bool dual_fits_registers(bool count);
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
 }  // namespace rtg
 
@@ -1009,7 +1010,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     const char* e = std::getenv("RTG_DUAL");
     const char* ew = std::getenv("RTG_LDS_WAVES");
     if (dj.lds_waves == kLdsWaves && stk16 && !dscene.tex_full && !(e && std::atoi(e) == 0) &&
-        !(ew && std::atoi(ew) == 16)) {
+        !(ew && std::atoi(ew) == 16) && dual_fits_registers((job->flags & RTG_RENDER_COUNT) != 0)) {
       for (const int f4 : {3, 2}) {
         DevJob a = dj, b = dj;
         a.lds_sphere_f4 = b.lds_sphere_f4 = f4;

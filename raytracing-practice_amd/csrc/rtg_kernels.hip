@@ -1605,6 +1605,23 @@ hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J,
   }
 }
 
+// The dual launch (rtg_api.cpp) needs the 16-wave kernel's four waves and the 4-wave kernel's one
+// wave of a SIMD to fit its 512 registers per lane together (allocation granule 8): checked on the
+// compiled kernels, so a later change that grows either one drops the dual launch instead of leaving
+// its second workgroup to run after the first has taken all the work.
+bool dual_fits_registers(bool count) {
+  auto alloc = [](const void* fn) {
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, fn) != hipSuccess) return 1 << 20;
+    return (a.numRegs + 7) / 8 * 8;
+  };
+  const void* k16 = count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, kLdsWaves, 4, false, kGeomLds>)
+                          : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, kLdsWaves, 4, false, kGeomLds>);
+  const void* k4 = count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds>)
+                         : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds>);
+  return 4 * alloc(k16) + alloc(k4) <= 512;
+}
+
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,
                           hipStream_t stream) {
   if (n_pixels <= 0) return hipSuccess;

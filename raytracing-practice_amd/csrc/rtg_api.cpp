@@ -983,8 +983,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   // stack entries of the persistent LDS schedule: 16-bit for 4-wide trees whose leaf codes fit 16 bits
   // and whose stack needs no spill (kernel LdsStack16), else 32-bit
   const char* lds_entries_env = std::getenv("RTG_STACK_LDS_ENTRIES");
-  const bool stk16 = dscene.node_width == 4 && dscene.num_refs <= 4096 && need <= kLdsStack && !lds_entries_env &&
-                     !dscene.tex_full;
+  const bool stk16 = dscene.node_width == 4 && dscene.num_refs <= 4096 && dscene.num_nodes * 112 <= 32768 &&
+                     need <= kLdsStack && !lds_entries_env && !dscene.tex_full;
   dj.stack_esz = stk16 ? 2 : 4;
   dj.lds_waves = kLdsWaves;
   int lds_bytes = lds_layout(dscene, kLdsStack, kLdsWaves, dj.stack_esz, &dj);
@@ -1107,11 +1107,12 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (skip_kernel || variant != 3) lds4 = -1;
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
-                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm};
+                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks};
     j4 = dj;
     j4.lds_waves = 4;
     j4.lds_nodes = l4[0], j4.lds_refs = l4[1], j4.lds_spheres = l4[2], j4.lds_quads = l4[3];
     j4.lds_materials = l4[4], j4.lds_textures = l4[5], j4.lds_perlin_vec = l4[6], j4.lds_perlin_perm = l4[7];
+    j4.lds_stacks = l4[8];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
   if (lds4 > 0) {

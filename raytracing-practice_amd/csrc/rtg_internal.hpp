@@ -191,6 +191,7 @@ struct DevJob {
   int32_t lds_sphere_f4;                     // float4s per sphere record in the LDS copy (2 or 3)
   int32_t lds_waves;                         // persistent LDS kernel: waves per workgroup
   int32_t stack_esz;                         // persistent kernels: bytes per LDS stack entry (2 or 4)
+  int32_t lds_stacks;                        // persistent kernels: byte offset of the traversal stacks in LDS
 
 };
 

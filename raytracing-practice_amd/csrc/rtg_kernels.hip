@@ -231,10 +231,11 @@ struct LdsStack {
   __device__ __forceinline__ void store(int32_t sp, int32_t v) const { lds[sp * 64] = v; }
   __device__ __forceinline__ int32_t load(int32_t sp) const { return lds[sp * 64]; }
 };
-// LdsStack16: 16-bit entries for the LDS schedule of 4-wide trees (inner-node codes are LDS byte
-// addresses / 16 < 10240, leaf codes ~((first << 3) | (count - 1)) with first < 4096 — the host
-// checks): half the LDS of 32-bit entries, which is what lets a second persistent launch share the
-// CU with book-1 (DESIGN.md §3 "occupancy").
+// LdsStack16: 16-bit entries for the LDS schedule of 4-wide trees whose codes fit an int16: the node
+// array sits at LDS address 0, so inner-node codes (absolute LDS byte addresses) stay below 32768
+// for trees of <= 292 nodes, and leaf codes ~((first << 3) | (count - 1)) need first < 4096 (the host
+// checks both, the kernel re-checks the node range): half the LDS of 32-bit entries, which is what
+// lets a second persistent launch share the CU with book-1 (DESIGN.md §3 "occupancy").
 template <int N>
 struct LdsStack16 {
   int16_t* lds;
@@ -389,8 +390,7 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
   const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
-  // LDS scenes: inner-node codes are the node's LDS byte address / 16 (nodes are 16-byte aligned)
-  const uint32_t na = GEOM == kGeomLds ? static_cast<uint32_t>(t.todo) << 4 : static_cast<uint32_t>(t.todo);
+  const uint32_t na = static_cast<uint32_t>(t.todo);  // LDS scenes: the node's LDS address
   nf4 nx, ny, nz, fx, fy, fz;
   int4 cc;
   if constexpr (GEOM == kGeomLds) {
@@ -1203,8 +1203,8 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  int32_t* lstk = reinterpret_cast<int32_t*>(smem) + wave * STACK * 64 + lane;
-  int16_t* lstk16 = reinterpret_cast<int16_t*>(smem) + wave * STACK * 64 + lane;
+  int32_t* lstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
+  int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
   if constexpr (GEOM == kGeomTreelet) {
     float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
     for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += WAVES * 64) l_top[k] = S.nodes[k];
@@ -1239,12 +1239,12 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) unsigned char*)smem))) + J.lds_nodes;
   for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) {
     float4 v = S.nodes[k];
-    if (WIDE == 4 && k % 7 == 6) {  // code row: inner-node codes become absolute LDS addresses / 16
+    if (WIDE == 4 && k % 7 == 6) {  // code row: inner-node codes become absolute LDS addresses
       int4 c = *reinterpret_cast<int4*>(&v);
-      c.x = c.x >= 0 ? (c.x + node_rebase) >> 4 : c.x;
-      c.y = c.y >= 0 ? (c.y + node_rebase) >> 4 : c.y;
-      c.z = c.z >= 0 ? (c.z + node_rebase) >> 4 : c.z;
-      c.w = c.w >= 0 ? (c.w + node_rebase) >> 4 : c.w;
+      c.x = c.x >= 0 ? c.x + node_rebase : c.x;
+      c.y = c.y >= 0 ? c.y + node_rebase : c.y;
+      c.z = c.z >= 0 ? c.z + node_rebase : c.z;
+      c.w = c.w >= 0 ? c.w + node_rebase : c.w;
       v = *reinterpret_cast<float4*>(&c);
     }
     l_nodes[k] = v;
@@ -1265,9 +1265,13 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
-  if (WIDE == 4) {  // inner-node codes are absolute LDS byte addresses / 16
-    L.root_code = node_rebase >> 4;
-    L.node_limit = (node_rebase + static_cast<int32_t>(S.num_nodes) * 112) >> 4;
+  if (WIDE == 4) {  // inner-node codes are absolute LDS byte addresses
+    L.root_code = node_rebase;
+    L.node_limit = node_rebase + static_cast<int32_t>(S.num_nodes) * 112;
+  }
+  if (STK16 && L.node_limit > 32768) {  // codes would not fit the 16-bit stack: report, render nothing
+    if (threadIdx.x == 0) atomicAdd(&J.counters[5], 1ull);
+    return;
   }
   L.refs = l_refs;
   L.spheres = l_spheres;
@@ -1541,9 +1545,12 @@ int kernel_stack_depth(int bvh_depth) {
 // one CU's 160 KiB; fills the scene-copy offsets of the job.
 int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   auto a16 = [](int64_t x) { return (x + 15) & ~int64_t(15); };
-  int64_t off = a16(int64_t(waves) * stack * 64 * esz);  // traversal stacks (esz bytes per entry)
-  const int64_t nodes = off;
-  off = a16(off + S.num_nodes * (S.node_width == 4 ? 112 : 64));
+  // the node array first (at LDS address 0: inner-node codes are its byte offsets, <= 15 bits for
+  // trees of <= 292 4-wide nodes, LdsStack16), then the traversal stacks (esz bytes per entry)
+  const int64_t nodes = 0;
+  int64_t off = a16(S.num_nodes * (S.node_width == 4 ? 112 : 64));
+  const int64_t stacks = off;
+  off = a16(off + int64_t(waves) * stack * 64 * esz);
   const int64_t spheres = off;
   off = a16(off + S.num_spheres * 16 * (J ? J->lds_sphere_f4 : 3));
   const int64_t quads = off;
@@ -1563,6 +1570,7 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
     J->lds_materials = static_cast<int32_t>(materials);
     J->lds_textures = static_cast<int32_t>(textures);
     J->lds_nodes = static_cast<int32_t>(nodes);
+    J->lds_stacks = static_cast<int32_t>(stacks);
     J->lds_spheres = static_cast<int32_t>(spheres);
     J->lds_quads = static_cast<int32_t>(quads);
     J->lds_refs = static_cast<int32_t>(refs);
@@ -1581,6 +1589,7 @@ int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
   const int64_t nodes = std::min<int64_t>(S->num_nodes, room / 112);
   S->treelet_bytes = static_cast<int32_t>(nodes * 112);
   J->lds_nodes = static_cast<int32_t>(stacks);
+  J->lds_stacks = 0;
   return static_cast<int>(stacks + nodes * 112);
 }
 

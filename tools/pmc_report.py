@@ -59,10 +59,20 @@ def main():
         if not os.path.exists(p):
             continue
         per, meta = load(p, a.kernel)
+        # the render kernel that did the frame's work: the longest non-COUNT dispatch name (a dual
+        # launch's 4-wave partner, serialised by counter collection, finds the work done and ends in
+        # microseconds; tools/profile.sh takes the PMC passes with RTG_DUAL=0 for that reason)
+        durs = {}
+        for d in per:
+            if not (a.timed_only and is_count_variant(meta[d][0])):
+                durs.setdefault(meta[d][0], []).append(meta[d][3])
+        if not durs:
+            continue
+        main = max(durs, key=lambda n: sum(durs[n]) / len(durs[n]))
         for d, vals in per.items():
             name = meta[d][0]
-            if a.timed_only and is_count_variant(name):
-                continue  # RTG_RENDER_COUNT variant
+            if name != main:
+                continue
             for k, v in vals.items():
                 counters.setdefault(k, []).append(v)
             info[sub] = meta[d]
@@ -110,6 +120,8 @@ def main():
         rec = {"workload": a.workload, "kernel_ns": round(ns_avg),
                **{k: out[k] for k in keys if k in out},
                "vgpr": next(iter(out["dispatch"].values()))["vgpr"] if out["dispatch"] else None,
+               "launch": "the 16-wave persistent launch alone (RTG_DUAL=0): counter collection serialises the "
+                         "dual launch's two dispatches (DESIGN.md §6)",
                "source": "rocprofv3 --pmc passes of tools/profile.sh (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU, "
                          "SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY, "
                          "SQ_LDS_BANK_CONFLICT, SQ_ACTIVE_INST_LDS, GRBM_GUI_ACTIVE, TCC_HIT/MISS)",

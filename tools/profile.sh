@@ -10,6 +10,9 @@ OUT=gpurun_out/prof
 mkdir -p "$OUT"
 BENCH=(python3 bench.py --steps "${STEPS:-3}" --warmup 1 --no-cpu-baseline "$@")
 PMC_BENCH=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@")
+# counter collection serialises dispatches: a dual launch's second persistent kernel
+# would only start after the first had taken all the work, so the PMC passes profile the single
+# 16-wave launch (RTG_DUAL=0); the trace pass above times the shipped dual launch
 run() {  # name timeout rocprofv3-args...
   local name=$1 t=$2
   shift 2
@@ -22,6 +25,7 @@ run() {  # name timeout rocprofv3-args...
 }
 run trace 600 --kernel-trace --stats -S --summary-output-file summary \
     -f csv -d "$OUT/trace" -o run -- "${BENCH[@]}" || exit $?
+export RTG_DUAL=0
 run pmc_fetch 600 --pmc FETCH_SIZE -f csv -d "$OUT/pmc_fetch" -o run -- "${PMC_BENCH[@]}" || exit $?
 run pmc_write 600 --pmc WRITE_SIZE -f csv -d "$OUT/pmc_write" -o run -- "${PMC_BENCH[@]}" || exit $?
 run pmc_sq 600 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS \

@@ -59,6 +59,16 @@ def test_book1_config1(gpu_lib, scenes, oracle):
     assert 2.0 < st.segments / st.samples < 3.2  # 2.55 segments/sample at depth 10
 
 
+@pytest.mark.parametrize("grid", [13, 14])
+def test_lds_scene_with_32bit_stack_codes(gpu_lib, scenes, oracle, grid):
+    """Bouncing-sphere grids of half-width 13 and 14 still fit the LDS schedule but their 4-wide trees
+    have more than 292 nodes, so node codes (LDS addresses) no longer fit a 16-bit stack entry: the
+    schedule keeps 32-bit entries there (and no dual launch); the frame must still match the oracle."""
+    g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", grid=grid, image_width=96,
+                             aspect_ratio=16.0 / 9.0, samples_per_pixel=4, max_depth=20)
+    assert_parity(g, o, st, segs)
+
+
 @pytest.mark.parametrize("name,W,spp,depth,exact", [
     ("cornell_box", 96, 16, 50, 0.999),
     ("quads", 64, 8, 50, 0.999),

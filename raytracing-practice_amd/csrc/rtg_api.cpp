@@ -1105,6 +1105,10 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
             "hipMemsetAsync(partial sums)");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
   if (skip_kernel || variant != 3) lds4 = -1;
+  if (std::getenv("RTG_VERBOSE"))
+    std::fprintf(stderr, "[rtg] schedule %d: %d workgroups of %d waves, %d B LDS, stack %d x %d B, dual %s (%d B)\n",
+                 variant, grid_blocks, dj.lds_waves, lds_bytes, stack_depth, dj.stack_esz, lds4 > 0 ? "on" : "off",
+                 lds4);
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
                           j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks};
@@ -1116,7 +1120,15 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
   if (lds4 > 0) {
-    if (!s->aux_stream) RTG_HIP(hipStreamCreateWithFlags(&s->aux_stream, hipStreamNonBlocking), "hipStreamCreate");
+    // the aux launch must sit in a hardware queue of its own, or it only starts after the main launch
+    // has drained (HIP shares its GPU_MAX_HW_QUEUES = 4 queues round-robin among a process's streams:
+    // with RCCL or a second library's streams the two launches serialised, +10 %); high-priority
+    // streams are served from a separate queue pool
+    if (!s->aux_stream) {
+      int least = 0, greatest = 0;
+      RTG_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+      RTG_HIP(hipStreamCreateWithPriority(&s->aux_stream, hipStreamNonBlocking, greatest), "hipStreamCreate");
+    }
     if (!s->ev_fork) RTG_HIP(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming), "hipEventCreate");
     if (!s->ev_join) RTG_HIP(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming), "hipEventCreate");
     RTG_HIP(hipEventRecord(s->ev_fork, stream), "hipEventRecord");

@@ -21,6 +21,8 @@
 // fused ops are the slab tests, which only cull (boxes are rounded outward on the host).
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 
 #include "rtg_internal.hpp"
 
@@ -45,9 +47,41 @@ __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y 
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
   return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+// Correctly rounded fp32 division and square root without the compiler's special-case steps.
+// div_rn is the IEEE sequence hipcc emits for `x / y` (rcp, two refinements of the reciprocal and
+// of the quotient) minus v_div_scale / v_div_fmas / v_div_fixup, which change nothing unless an
+// operand or the quotient lies within 2^64 of the fp32 range ends (or is 0, inf, NaN): in range
+// the results are the same bits, 8 VALU instead of 11. Every call site divides by a ray length,
+// a radius, a refraction index or a quad denominator (>= 1e-8), and a numerator that is tiny or
+// zero yields a root far below tmin either way.
+__device__ __forceinline__ float div_rn(float x, float y) {
+  const float r0 = __builtin_amdgcn_rcpf(y);
+  const float e0 = fmaf(-y, r0, 1.0f);
+  const float r = fmaf(e0, r0, r0);
+  const float q0 = x * r;
+  const float e1 = fmaf(-y, q0, x);
+  const float q1 = fmaf(e1, r, q0);
+  const float e2 = fmaf(-y, q1, x);
+  return fmaf(e2, r, q1);
+}
+// sqrt_rn: the compiler's correctly rounded sqrt (v_sqrt_f32, then the neighbour whose residual
+// changes sign) without its 2^32 pre-scaling of x < 2^-96 and its 0/inf class fix-up: exact for x
+// == 0 and 2^-96 <= x < inf, 9 VALU instead of 16. Call sites: 1 - z^2 of a 24-bit uniform, a
+// 24-bit uniform, 1 - cos^2 and |1 - |perp|^2| (each 0 or >= 2^-25), and |v|^2 of ray directions
+// (camera rays, and scatter directions kept >= 1e-8 per axis by near_zero). The sphere test's
+// discriminant, which can be arbitrarily small, keeps sqrtf.
+__device__ __forceinline__ float sqrt_rn(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float lo = __int_as_float(__float_as_int(s) - 1);
+  const float hi = __int_as_float(__float_as_int(s) + 1);
+  const float rlo = fmaf(-lo, s, x);
+  const float rhi = fmaf(-hi, s, x);
+  const float t = rlo <= 0.0f ? lo : s;
+  return rhi > 0.0f ? hi : t;
+}
 __device__ __forceinline__ V3 unit(V3 a) {  // unit_vector: v / v.length() == (1/len) * v
-  const float len = sqrtf(dot(a, a));
-  return scl(1.0f / len, a);
+  const float len = sqrt_rn(dot(a, a));
+  return scl(div_rn(1.0f, len), a);
 }
 __device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
 __device__ __forceinline__ int ibits(float f) { return __float_as_int(f); }
@@ -98,7 +132,7 @@ __device__ __forceinline__ void sincos_turn(float u, float& sn, float& cs) {
 // unluckiest lane (~5 tries for 30 lanes at acceptance pi/6); this costs two draws, always.
 __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
   const float z = 1.0f - 2.0f * uniform(s);
-  const float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  const float r = sqrt_rn(fmaxf(0.0f, 1.0f - z * z));
   float sn, cs;
   sincos_turn(uniform(s), sn, cs);
   return v3(r * cs, r * sn, z);
@@ -143,7 +177,7 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float q = -(hb + copysignf(sq, hb));
   if (q == 0.0f || a == 0.0f) return -1.0f;
   const float t0 = q * inv_a;
-  const float t1 = c / q;
+  const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
   if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
@@ -161,7 +195,7 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   const double dn = static_cast<double>(n.x) * o.x + static_cast<double>(n.y) * o.y +
                     static_cast<double>(n.z) * o.z;
   const float num = static_cast<float>(static_cast<double>(q0.w) - dn);
-  const float t = num / denom;
+  const float t = div_rn(num, denom);
   if (!(tmin <= t && t <= tmax)) return -1.0f;
   const V3 p = add(o, scl(t, d));
   const V3 hp = sub(p, xyz(q0));
@@ -209,7 +243,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.sy = (static_cast<uint32_t>(ibits(t.iy)) >> 31) * 48;
   t.sz = (static_cast<uint32_t>(ibits(t.iz)) >> 31) * 48;
   t.a = dot(d, d);
-  t.inv_a = 1.0f / t.a;
+  t.inv_a = div_rn(1.0f, t.a);
   t.ox = -o.x * t.ix;
   t.oy = -o.y * t.iy;
   t.oz = -o.z * t.iz;
@@ -542,7 +576,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
   const V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y),
                     __builtin_amdgcn_rcpf(d.z));
   const V3 oi = v3(-o.x * inv.x, -o.y * inv.y, -o.z * inv.z);
-  const float a = dot(d, d), inv_a = 1.0f / a;
+  const float a = dot(d, d), inv_a = div_rn(1.0f, a);
   int sp = 0;
   int32_t todo = 0;
   while (true) {
@@ -744,7 +778,7 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
   V3 origin = v3(C.center[0], C.center[1], C.center[2]);
   if (C.defocus) {
     // random_in_unit_disk (vec3.hpp:158-169), direct: radius sqrt(U), angle from a second U
-    const float r = sqrtf(uniform(ps.rng));
+    const float r = sqrt_rn(uniform(ps.rng));
     float sn, cs;
     sincos_turn(uniform(ps.rng), sn, cs);
     const float px = r * cs, py = r * sn;
@@ -773,7 +807,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
     const float4 s0 = s[0], s1 = s[1];
     const V3 C = v3(s0.x + ps.time * s1.x, s0.y + ps.time * s1.y, s0.z + ps.time * s1.z);
     p = add(ps.o, scl(t, ps.d));
-    outward = scl(1.0f / s0.w, sub(p, C));
+    outward = scl(div_rn(1.0f, s0.w), sub(p, C));
     mat = ibits(s1.w);
   } else {
     const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
@@ -798,8 +832,8 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   auto sphere_uv = [&]() {
     const float theta = acosf(-outward.y);
     const float phi = atan2f(-outward.z, outward.x) + kPi;
-    u = phi / (2.0f * kPi);
-    v = theta / kPi;
+    u = div_rn(phi, 2.0f * kPi);
+    v = div_rn(theta, kPi);
   };
 
   if (type == RTG_MAT_DIFFUSE_LIGHT) {
@@ -829,14 +863,14 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   } else if (type == RTG_MAT_DIELECTRIC) {
     att = v3(1.0f, 1.0f, 1.0f);
     const float eta = m0.w;
-    const float ri = front ? (1.0f / eta) : eta;
+    const float ri = front ? div_rn(1.0f, eta) : eta;
     const V3 ud = unit(ps.d);
     const float cos_t = fminf(dot(neg(ud), n), 1.0f);
-    const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+    const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
     const bool cannot = ri * sin_t > 1.0f;
     bool reflect = cannot;
     if (!cannot) {
-      float r0 = (1.0f - ri) / (1.0f + ri);
+      float r0 = div_rn(1.0f - ri, 1.0f + ri);
       r0 = r0 * r0;
       const float x = 1.0f - cos_t;
       const float refl = r0 + (1.0f - r0) * (x * x * x * x * x);
@@ -847,7 +881,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
     } else {
       const float ct = fminf(dot(neg(ud), n), 1.0f);
       const V3 perp = scl(ri, add(ud, scl(ct, n)));
-      const V3 par = scl(-sqrtf(fabsf(1.0f - dot(perp, perp))), n);
+      const V3 par = scl(-sqrt_rn(fabsf(1.0f - dot(perp, perp))), n);
       dir = add(perp, par);
     }
   } else {
@@ -1621,7 +1655,10 @@ hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J,
 bool dual_fits_registers(bool count) {
   auto alloc = [](const void* fn) {
     hipFuncAttributes a{};
-    if (hipFuncGetAttributes(&a, fn) != hipSuccess) return 1 << 20;
+    const hipError_t err = hipFuncGetAttributes(&a, fn);
+    if (std::getenv("RTG_VERBOSE"))
+      std::fprintf(stderr, "[rtg] dual check: %s numRegs %d\n", hipGetErrorString(err), a.numRegs);
+    if (err != hipSuccess) return 1 << 20;
     return (a.numRegs + 7) / 8 * 8;
   };
   const void* k16 = count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, kLdsWaves, 4, false, kGeomLds>)

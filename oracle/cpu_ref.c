@@ -661,10 +661,14 @@ static inline f3 fv_sub(f3 a, f3 b) { return F3(a.x - b.x, a.y - b.y, a.z - b.z)
 static inline f3 fmul3(f3 a, f3 b) { return F3(a.x * b.x, a.y * b.y, a.z * b.z); }
 static inline f3 fscl(float t, f3 a) { return F3(t * a.x, t * a.y, t * a.z); }
 static inline f3 fneg(f3 a) { return F3(-a.x, -a.y, -a.z); }
-static inline float fdot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* fused multiply-adds of the spec (round 2): the same fmaf chains, in the same order,
+   as rtg_kernels.hip dot / cross / madd / vfma */
+static inline float fdot(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 static inline f3 fcross(f3 a, f3 b) {
-  return F3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return F3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
 }
+static inline f3 fmadd3(float t, f3 a, f3 b) { return F3(fmaf(t, a.x, b.x), fmaf(t, a.y, b.y), fmaf(t, a.z, b.z)); }
+static inline f3 fvfma(f3 a, f3 b, f3 c) { return F3(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z)); }
 static inline f3 funit(f3 a) { return fscl(1.0f / sqrtf(fdot(a, a)), a); }
 static inline f3 fd(const double v[3]) { return F3((float)v[0], (float)v[1], (float)v[2]); }
 
@@ -693,7 +697,7 @@ uint64_t orc_rng_state(uint64_t seed, uint32_t pixel, uint32_t sample) {
 float orc_rng_uniform(uint64_t* state) { return U(state); }
 
 /* sin and cos of 2*pi*u, u in [0,1) (DESIGN.md rtg-f32 "direct sampling"): quadrant reduction and
-   Taylor polynomials on [-pi/4, pi/4), plain fp32 multiply/add only (no libm), so the GPU kernel
+   Taylor polynomials on [-pi/4, pi/4), plain fp32 multiply / fmaf only (no libm), so the GPU kernel
    (rtg_kernels.hip sincos_turn) reproduces every bit. Used instead of the reference's rejection
    loops (vec3.hpp:158-184), which make a wavefront wait for its unluckiest lane. */
 static void sincos_turn(float u, float* sn, float* cs) {
@@ -701,9 +705,11 @@ static void sincos_turn(float u, float* sn, float* cs) {
   float q = floorf(t);
   float x = (t - q - 0.5f) * 1.57079637f;
   float x2 = x * x;
-  float sx = x + x * x2 * (-1.66666672e-1f + x2 * (8.33333377e-3f + x2 * (-1.98412701e-4f + x2 * 2.75573188e-6f)));
-  float cx = 1.0f + x2 * (-0.5f + x2 * (4.16666679e-2f + x2 * (-1.38888892e-3f +
-                                                              x2 * (2.48015876e-5f + x2 * -2.75573188e-7f))));
+  float ps = fmaf(x2, fmaf(x2, fmaf(x2, 2.75573188e-6f, -1.98412701e-4f), 8.33333377e-3f), -1.66666672e-1f);
+  float sx = fmaf(x * x2, ps, x);
+  float pc = fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, -2.75573188e-7f, 2.48015876e-5f), -1.38888892e-3f), 4.16666679e-2f),
+                  -0.5f);
+  float cx = fmaf(x2, pc, 1.0f);
   float a = (sx + cx) * 0.707106769f; /* sin(pi/4 + x) */
   float b = (cx - sx) * 0.707106769f; /* cos(pi/4 + x) */
   int qi = (int)q;
@@ -715,7 +721,7 @@ static void sincos_turn(float u, float* sn, float* cs) {
 /* random_unit_vector (vec3.hpp:172-184), direct: z = 1 - 2U, then the azimuth from a second U */
 static f3 f32_random_unit_vector(uint64_t* s) {
   float z = 1.0f - 2.0f * U(s);
-  float r = sqrtf(fmaxf(0.0f, 1.0f - z * z));
+  float r = sqrtf(fmaxf(0.0f, fmaf(-z, z, 1.0f)));
   float sn, cs;
   sincos_turn(U(s), &sn, &cs);
   return F3(r * cs, r * sn, z);
@@ -835,22 +841,22 @@ static void world32_free(world32* w) {
    off the surface, and a grazing ray's own root c/q can exceed tmin = 0.001: a chrome sphere's
    reflection then re-hits the sphere from inside and stays trapped until max_depth. */
 static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, float tmax, int origin) {
-  f3 C = F3(s[0] + time * s[4], s[1] + time * s[5], s[2] + time * s[6]);
+  f3 C = fmadd3(time, F3(s[4], s[5], s[6]), F3(s[0], s[1], s[2]));
   f3 oc = fv_sub(o, C);
   float a = fdot(d, d), inv_a = 1.0f / a; /* per ray on the GPU (Trav::a, inv_a) */
   float hb = fdot(oc, d);
   float c, disc;
   if (fabsf(s[3]) < 16.0f) {
     /* disc = a (r^2 - |oc - (h/a) d|^2), 1/a rounded first */
-    c = fdot(oc, oc) - s[3] * s[3];
+    c = fmaf(-s[3], s[3], fdot(oc, oc));
     float sh = hb * inv_a;
-    f3 f = F3(oc.x - sh * d.x, oc.y - sh * d.y, oc.z - sh * d.z);
-    disc = a * (s[3] * s[3] - fdot(f, f));
+    f3 f = fmadd3(-sh, d, oc);
+    disc = a * fmaf(s[3], s[3], -fdot(f, f));
   } else {
     double ox = (double)o.x - (double)C.x, oy = (double)o.y - (double)C.y,
            oz = (double)o.z - (double)C.z, r = (double)s[3];
     c = (float)((ox * ox + oy * oy + oz * oz) - r * r);
-    disc = hb * hb - a * c;
+    disc = fmaf(hb, hb, -(a * c));
   }
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);
@@ -871,7 +877,7 @@ static float quad_t32(const float* q, f3 o, f3 d, float tmin, float tmax) {
   double dn = (double)n.x * o.x + (double)n.y * o.y + (double)n.z * o.z;
   float t = (float)((double)q[3] - dn) / denom;
   if (!(tmin <= t && t <= tmax)) return -1.0f;
-  f3 p = fv_add(o, fscl(t, d));
+  f3 p = fmadd3(t, d, o);
   f3 hp = fv_sub(p, F3(q[0], q[1], q[2]));
   f3 w = F3(q[10], q[11], q[12]);
   float alpha = fdot(w, fcross(hp, F3(q[7], q[8], q[9])));
@@ -915,7 +921,7 @@ static float perlin_noise32(const float* vec, const rtg_perlin* pl, f3 p) {
         f3 c = F3(vec[idx * 3], vec[idx * 3 + 1], vec[idx * 3 + 2]);
         f3 wv = F3(u - di, v - dj, w - dk);
         float fu = di ? uu : (1.0f - uu), fv = dj ? vv : (1.0f - vv), fw = dk ? ww : (1.0f - ww);
-        accum += fu * fv * fw * fdot(c, wv);
+        accum = fmaf(fu * fv * fw, fdot(c, wv), accum);
       }
   return accum;
 }
@@ -949,12 +955,12 @@ static f3 tex_value32(const world32* w, int32_t t, float u, float v, f3 p) {
       float accum = 0.0f, weight = 1.0f;
       f3 tp = p;
       for (int o = 0; o < 7; ++o) {
-        accum += weight * perlin_noise32(vec, pl, tp);
+        accum = fmaf(weight, perlin_noise32(vec, pl, tp), accum);
         weight *= 0.5f;
         tp = fscl(2.0f, tp);
       }
       float tb = fabsf(accum);
-      float sv = 0.5f * (1.0f + sinf(tf[0] * p.z + 10.0f * tb));
+      float sv = 0.5f * (1.0f + sinf(fmaf(tf[0], p.z, 10.0f * tb)));
       return F3(sv, sv, sv);
     }
     break;
@@ -978,12 +984,12 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
   f3 center = F3(cf[9], cf[10], cf[11]);
   float ox = U(&st) - 0.5f;
   float oy = U(&st) - 0.5f;
-  f3 ps = fv_add(fv_add(p00, fscl((float)i + ox, du)), fscl((float)j + oy, dvv));
+  f3 ps = fmadd3((float)j + oy, dvv, fmadd3((float)i + ox, du, p00));
   f3 o = center;
   if (!(cam->defocus_angle <= 0.0f)) {
     float px, py;
     f32_random_in_unit_disk(&st, &px, &py);
-    o = fv_add(fv_add(center, fscl(px, F3(cf[12], cf[13], cf[14]))), fscl(py, F3(cf[15], cf[16], cf[17])));
+    o = fmadd3(py, F3(cf[15], cf[16], cf[17]), fmadd3(px, F3(cf[12], cf[13], cf[14]), center));
   }
   f3 d = fv_sub(ps, o);
   float time = U(&st);
@@ -999,16 +1005,16 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
       node_hit32(w, 0, o, d, O, Dd, time, origin, &tbest, &best);
     }
     if (best < 0) {
-      L = fv_add(L, fmul3(T, bg));
+      L = fvfma(T, bg, L);
       break;
     }
     const rtg_primitive* pr = &w->s->prims[best];
-    f3 p = fv_add(o, fscl(tbest, d)), outward;
+    f3 p = fmadd3(tbest, d, o), outward;
     float u = 0.0f, v = 0.0f;
     int sphere = pr->kind == RTG_PRIM_SPHERE;
     if (sphere) {
       const float* s = w->sph + best * 8;
-      f3 C = F3(s[0] + time * s[4], s[1] + time * s[5], s[2] + time * s[6]);
+      f3 C = fmadd3(time, F3(s[4], s[5], s[6]), F3(s[0], s[1], s[2]));
       outward = fscl(1.0f / s[3], fv_sub(p, C));
     } else {
       const float* q = w->qd + best * 16;
@@ -1032,16 +1038,16 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
     }
     f3 att, dir;
     if (m->type == RTG_MAT_DIFFUSE_LIGHT) {
-      L = fv_add(L, fmul3(T, tex_value32(w, m->texture, u, v, p)));
+      L = fvfma(T, tex_value32(w, m->texture, u, v, p), L);
       break;
     } else if (m->type == RTG_MAT_LAMBERTIAN) {
       dir = fv_add(n, f32_random_unit_vector(&st));
       if (fabsf(dir.x) < 1e-8f && dir.y < 1e-8f && fabsf(dir.z) < 1e-8f) dir = n;
       att = tex_value32(w, m->texture, u, v, p);
     } else if (m->type == RTG_MAT_METAL) {
-      f3 refl = fv_sub(d, fscl(2.0f * fdot(d, n), n));
+      f3 refl = fmadd3(-(2.0f * fdot(d, n)), n, d);
       f3 r = f32_random_unit_vector(&st);
-      dir = fv_add(funit(refl), fscl(mf[0], r));
+      dir = fmadd3(mf[0], r, funit(refl));
       att = F3(mf[2], mf[3], mf[4]);
       if (!(fdot(dir, n) > 0.0f)) break;
     } else if (m->type == RTG_MAT_DIELECTRIC) {
@@ -1049,23 +1055,22 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
       float ri = front ? (1.0f / mf[1]) : mf[1];
       f3 ud = funit(d);
       float ct = fminf(fdot(fneg(ud), n), 1.0f);
-      float stt = sqrtf(1.0f - ct * ct);
+      float stt = sqrtf(fmaf(-ct, ct, 1.0f));
       int cannot = ri * stt > 1.0f;
       int reflect = cannot;
       if (!cannot) {
         float r0 = (1.0f - ri) / (1.0f + ri);
         r0 = r0 * r0;
         float x = 1.0f - ct;
-        float refl = r0 + (1.0f - r0) * (x * x * x * x * x);
+        float refl = fmaf(1.0f - r0, x * x * x * x * x, r0);
         reflect = refl > U(&st);
       }
       if (reflect) {
-        dir = fv_sub(ud, fscl(2.0f * fdot(ud, n), n));
+        dir = fmadd3(-(2.0f * fdot(ud, n)), n, ud);
       } else {
         float c2 = fminf(fdot(fneg(ud), n), 1.0f);
-        f3 perp = fscl(ri, fv_add(ud, fscl(c2, n)));
-        f3 par = fscl(-sqrtf(fabsf(1.0f - fdot(perp, perp))), n);
-        dir = fv_add(perp, par);
+        f3 perp = fscl(ri, fmadd3(c2, n, ud));
+        dir = fmadd3(-sqrtf(fabsf(1.0f - fdot(perp, perp))), n, perp);
       }
     } else {
       break;

@@ -17,8 +17,9 @@
 // laid out [depth][lane] (bank-conflict-free for ds_read_b32/ds_write_b32).
 //
 // Numerics: the fp32 spec in DESIGN.md ("rtg-f32"); compiled with -ffp-contract=off so every
-// expression rounds as written and matches the CPU restatement in oracle/cpu_ref.c. The only
-// fused ops are the slab tests, which only cull (boxes are rounded outward on the host).
+// expression rounds as written and matches the CPU restatement in oracle/cpu_ref.c. Fused ops are
+// explicit fmaf calls (dot / cross / madd / vfma and the forms marked in the code), placed exactly
+// as in the oracle; the slab tests' packed FMAs only cull (boxes are rounded outward on the host).
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
@@ -43,9 +44,18 @@ __device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ V3 scl(float t, V3 a) { return v3(t * a.x, t * a.y, t * a.z); }
 __device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// Fused multiply-adds of the rtg-f32 spec (round 2): dot products, cross products,
+// `b + t a` and the other forms below are single-rounding fmaf chains in exactly this order, here
+// and in oracle/cpu_ref.c (fmaf is correctly rounded on both sides, so the bits still agree).
+__device__ __forceinline__ float dot(V3 a, V3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {
-  return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+  return v3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+__device__ __forceinline__ V3 madd(float t, V3 a, V3 b) {  // b + t a
+  return v3(fmaf(t, a.x, b.x), fmaf(t, a.y, b.y), fmaf(t, a.z, b.z));
+}
+__device__ __forceinline__ V3 vfma(V3 a, V3 b, V3 c) {  // a * b + c per component
+  return v3(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z));
 }
 // Correctly rounded fp32 division and square root without the compiler's special-case steps.
 // div_rn is the IEEE sequence hipcc emits for `x / y` (rcp, two refinements of the reciprocal and
@@ -109,16 +119,18 @@ __device__ __forceinline__ float uniform(uint64_t& s) {  // random_double(), [0,
 }
 
 // sin and cos of 2*pi*u, u in [0,1): quadrant reduction and Taylor polynomials on [-pi/4, pi/4),
-// plain fp32 multiply/add only, so oracle/cpu_ref.c (sincos_turn) reproduces every bit.
+// plain fp32 multiply / fmaf only, so oracle/cpu_ref.c (sincos_turn) reproduces every bit.
 __device__ __forceinline__ void sincos_turn(float u, float& sn, float& cs) {
   const float t = 4.0f * u;
   const float q = floorf(t);
   const float x = (t - q - 0.5f) * 1.57079637f;
   const float x2 = x * x;
-  const float sx =
-      x + x * x2 * (-1.66666672e-1f + x2 * (8.33333377e-3f + x2 * (-1.98412701e-4f + x2 * 2.75573188e-6f)));
-  const float cx = 1.0f + x2 * (-0.5f + x2 * (4.16666679e-2f + x2 * (-1.38888892e-3f +
-                                                                      x2 * (2.48015876e-5f + x2 * -2.75573188e-7f))));
+  // Horner steps as fmaf (rtg-f32 round 2)
+  const float ps = fmaf(x2, fmaf(x2, fmaf(x2, 2.75573188e-6f, -1.98412701e-4f), 8.33333377e-3f), -1.66666672e-1f);
+  const float sx = fmaf(x * x2, ps, x);
+  const float pc = fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, -2.75573188e-7f, 2.48015876e-5f), -1.38888892e-3f),
+                                 4.16666679e-2f), -0.5f);
+  const float cx = fmaf(x2, pc, 1.0f);
   const float a = (sx + cx) * 0.707106769f;  // sin(pi/4 + x)
   const float b = (cx - sx) * 0.707106769f;  // cos(pi/4 + x)
   const int qi = static_cast<int>(q);
@@ -132,7 +144,7 @@ __device__ __forceinline__ void sincos_turn(float u, float& sn, float& cs) {
 // unluckiest lane (~5 tries for 30 lanes at acceptance pi/6); this costs two draws, always.
 __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
   const float z = 1.0f - 2.0f * uniform(s);
-  const float r = sqrt_rn(fmaxf(0.0f, 1.0f - z * z));
+  const float r = sqrt_rn(fmaxf(0.0f, fmaf(-z, z, 1.0f)));
   float sn, cs;
   sincos_turn(uniform(s), sn, cs);
   return v3(r * cs, r * sn, z);
@@ -152,25 +164,25 @@ constexpr float kSphereF64Radius = 16.0f;
 // only the near root c / q is a division.
 __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float a, float inv_a, float time,
                                           float tmin, float tmax, bool origin) {
-  const V3 C = v3(s0.x + time * s1.x, s0.y + time * s1.y, s0.z + time * s1.z);
+  const V3 C = madd(time, xyz(s1), xyz(s0));
   const V3 oc = sub(o, C);
   const float hb = dot(oc, d);
   float c, disc;
   if (fabsf(s0.w) < kSphereF64Radius) {
-    c = dot(oc, oc) - s0.w * s0.w;
+    c = fmaf(-s0.w, s0.w, dot(oc, oc));
     // disc = a (r^2 - |f|^2), f = oc - (h/a) d the centre-to-line offset: no h^2 - a c
     // cancellation, so a grazing ray far from a small sphere is classified to ~r^2 2^-22, not
     // ~h^2 2^-24 (a false hit outside the sphere's box, which box culling precision then decides)
     const float s = hb * inv_a;
-    const V3 f = v3(oc.x - s * d.x, oc.y - s * d.y, oc.z - s * d.z);
-    disc = a * (s0.w * s0.w - dot(f, f));
+    const V3 f = madd(-s, d, oc);
+    disc = a * fmaf(s0.w, s0.w, -dot(f, f));
   } else {
     const double ox = static_cast<double>(o.x) - static_cast<double>(C.x);
     const double oy = static_cast<double>(o.y) - static_cast<double>(C.y);
     const double oz = static_cast<double>(o.z) - static_cast<double>(C.z);
     const double r = static_cast<double>(s0.w);
     c = static_cast<float>((ox * ox + oy * oy + oz * oz) - r * r);
-    disc = hb * hb - a * c;
+    disc = fmaf(hb, hb, -(a * c));
   }
   if (disc < 0.0f) return -1.0f;
   const float sq = sqrtf(disc);
@@ -197,7 +209,7 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   const float num = static_cast<float>(static_cast<double>(q0.w) - dn);
   const float t = div_rn(num, denom);
   if (!(tmin <= t && t <= tmax)) return -1.0f;
-  const V3 p = add(o, scl(t, d));
+  const V3 p = madd(t, d, o);
   const V3 hp = sub(p, xyz(q0));
   const V3 u = xyz(q[1]), v = xyz(q[2]), w = xyz(q[3]);
   const float alpha = dot(w, cross(hp, v));
@@ -684,7 +696,7 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
         const float fu = di ? uu : (1.0f - uu);
         const float fv = dj ? vv : (1.0f - vv);
         const float fw = dk ? ww : (1.0f - ww);
-        accum += fu * fv * fw * dot(c, wv);
+        accum = fmaf(fu * fv * fw, dot(c, wv), accum);
       }
     }
   }
@@ -695,7 +707,7 @@ __device__ float perlin_turb(const float4* vec, const int32_t* perm, V3 p) {
   float accum = 0.0f, weight = 1.0f;
   V3 tp = p;
   for (int i = 0; i < 7; ++i) {
-    accum += weight * perlin_noise(vec, perm, tp);
+    accum = fmaf(weight, perlin_noise(vec, perm, tp), accum);
     weight *= 0.5f;
     tp = scl(2.0f, tp);
   }
@@ -745,7 +757,7 @@ __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3
       const float4* vec = S.perlin_vec + pt * 256;
       const int32_t* perm = S.perlin_perm + pt * 768;
       const float t = perlin_turb(vec, perm, p);
-      const float s = 0.5f * (1.0f + sinf(t0.w * p.z + 10.0f * t));
+      const float s = 0.5f * (1.0f + sinf(fmaf(t0.w, p.z, 10.0f * t)));
       return v3(s, s, s);
     }
     break;
@@ -774,7 +786,7 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
   const V3 p00 = v3(C.pixel00[0], C.pixel00[1], C.pixel00[2]);
   const V3 du = v3(C.du[0], C.du[1], C.du[2]);
   const V3 dv = v3(C.dv[0], C.dv[1], C.dv[2]);
-  const V3 sample_pt = add(add(p00, scl(fi, du)), scl(fj, dv));
+  const V3 sample_pt = madd(fj, dv, madd(fi, du, p00));
   V3 origin = v3(C.center[0], C.center[1], C.center[2]);
   if (C.defocus) {
     // random_in_unit_disk (vec3.hpp:158-169), direct: radius sqrt(U), angle from a second U
@@ -782,8 +794,7 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
     float sn, cs;
     sincos_turn(uniform(ps.rng), sn, cs);
     const float px = r * cs, py = r * sn;
-    origin = add(add(origin, scl(px, v3(C.defu[0], C.defu[1], C.defu[2]))),
-                 scl(py, v3(C.defv[0], C.defv[1], C.defv[2])));
+    origin = madd(py, v3(C.defv[0], C.defv[1], C.defv[2]), madd(px, v3(C.defu[0], C.defu[1], C.defu[2]), origin));
   }
   ps.o = origin;
   ps.d = sub(sample_pt, origin);
@@ -805,14 +816,14 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   if (sphere) {
     const float4* s = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
     const float4 s0 = s[0], s1 = s[1];
-    const V3 C = v3(s0.x + ps.time * s1.x, s0.y + ps.time * s1.y, s0.z + ps.time * s1.z);
-    p = add(ps.o, scl(t, ps.d));
+    const V3 C = madd(ps.time, xyz(s1), xyz(s0));
+    p = madd(t, ps.d, ps.o);
     outward = scl(div_rn(1.0f, s0.w), sub(p, C));
     mat = ibits(s1.w);
   } else {
     const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
     const float4 q0 = q[0];
-    p = add(ps.o, scl(t, ps.d));
+    p = madd(t, ps.d, ps.o);
     const V3 hp = sub(p, xyz(q0));
     const V3 w = xyz(q[3]);
     u = dot(w, cross(hp, xyz(q[2])));
@@ -839,7 +850,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
   if (type == RTG_MAT_DIFFUSE_LIGHT) {
     if (needs_uv) sphere_uv();
     const V3 e = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);  // < 0: solid colour inline
-    ps.L = add(ps.L, mul(ps.T, e));
+    ps.L = vfma(ps.T, e, ps.L);
     return false;
   }
   V3 dir, att;
@@ -855,8 +866,8 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
       att = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);
     } else {
       const V3 in = ps.d;
-      const V3 refl = sub(in, scl(2.0f * dot(in, n), n));
-      dir = add(unit(refl), scl(m0.z, r));
+      const V3 refl = madd(-(2.0f * dot(in, n)), n, in);
+      dir = madd(m0.z, r, unit(refl));
       att = xyz(m1);
       if (!(dot(dir, n) > 0.0f)) return false;  // absorbed: color_from_emission == 0
     }
@@ -866,23 +877,22 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
     const float ri = front ? div_rn(1.0f, eta) : eta;
     const V3 ud = unit(ps.d);
     const float cos_t = fminf(dot(neg(ud), n), 1.0f);
-    const float sin_t = sqrt_rn(1.0f - cos_t * cos_t);
+    const float sin_t = sqrt_rn(fmaf(-cos_t, cos_t, 1.0f));
     const bool cannot = ri * sin_t > 1.0f;
     bool reflect = cannot;
     if (!cannot) {
       float r0 = div_rn(1.0f - ri, 1.0f + ri);
       r0 = r0 * r0;
       const float x = 1.0f - cos_t;
-      const float refl = r0 + (1.0f - r0) * (x * x * x * x * x);
+      const float refl = fmaf(1.0f - r0, x * x * x * x * x, r0);
       reflect = refl > uniform(ps.rng);
     }
     if (reflect) {
-      dir = sub(ud, scl(2.0f * dot(ud, n), n));
+      dir = madd(-(2.0f * dot(ud, n)), n, ud);
     } else {
       const float ct = fminf(dot(neg(ud), n), 1.0f);
-      const V3 perp = scl(ri, add(ud, scl(ct, n)));
-      const V3 par = scl(-sqrt_rn(fabsf(1.0f - dot(perp, perp))), n);
-      dir = add(perp, par);
+      const V3 perp = scl(ri, madd(ct, n, ud));
+      dir = madd(-sqrt_rn(fabsf(1.0f - dot(perp, perp))), n, perp);
     }
   } else {
     return false;  // base material: scatter() == false, emitted() == 0
@@ -1154,7 +1164,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       ++w.segs;
       bool alive_path;
       if (tr.best < 0) {
-        ps.L = add(ps.L, mul(ps.T, bg));
+        ps.L = vfma(ps.T, bg, ps.L);
         alive_path = false;
       } else {
         if (COUNT) ++w.hits;
@@ -1358,7 +1368,7 @@ __global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCame
     ++segs;
     bool alive;
     if (tr.best < 0) {
-      ps.L = add(ps.L, mul(ps.T, bg));
+      ps.L = vfma(ps.T, bg, ps.L);
       alive = false;
     } else {
       if (COUNT) ++hits;
@@ -1410,7 +1420,7 @@ __global__ __launch_bounds__(256) void render_kernel_v0(DevScene S, DevCamera C,
     ++segs;
     bool alive;
     if (ref < 0) {
-      ps.L = add(ps.L, mul(ps.T, bg));
+      ps.L = vfma(ps.T, bg, ps.L);
       alive = false;
     } else {
       if (COUNT) ++hits;

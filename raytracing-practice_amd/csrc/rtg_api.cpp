@@ -46,6 +46,11 @@ constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
 constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
+// gfx950 allocates a workgroup's LDS in 1280-byte granules (160 KB = 128 of them): measured with the
+// dual launch, whose two workgroups stop sharing a CU exactly when the rounded sizes pass 160 KB
+constexpr int kLdsGranule = 1280;
+constexpr int kLdsPerCu = 160 * 1024;
+int lds_alloc(int bytes) { return (bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule; }
 }
 
 namespace {
@@ -314,6 +319,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->stack_need = bvh4.max_pushes;
     out->node_width = 4;
   }
+  if (std::getenv("RTG_VERBOSE"))
+    std::fprintf(stderr, "[rtg] bvh: %lld primitives, %zu binary nodes -> %lld nodes of width %d, depth %d, stack %d\n",
+                 static_cast<long long>(d->num_prims), bvh.nodes.size(), static_cast<long long>(out->num_nodes),
+                 out->node_width, out->depth, out->stack_need);
 
   // primitives, laid out in first-reference order for locality
   std::vector<int32_t> slot(d->num_prims, -1);
@@ -994,7 +1003,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     DevJob t = dj;
     const int b4 = lds_layout(dscene, kLdsStack, 4, dj.stack_esz, &t);
     if ((!e || std::atoi(e) == 4) && dscene.node_width == 4 && need <= kLdsStack && !lds_entries_env && b4 > 0 &&
-        b4 * kSmallSceneWgs <= 160 * 1024 && (stk16 || dscene.tex_full)) {
+        lds_alloc(b4) * kSmallSceneWgs <= kLdsPerCu && (stk16 || dscene.tex_full)) {
       dj = t;
       dj.lds_waves = 4;
       lds_bytes = b4;
@@ -1016,7 +1025,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
         a.lds_sphere_f4 = b.lds_sphere_f4 = f4;
         const int b16 = lds_layout(dscene, kLdsStack, kLdsWaves, 2, &a);
         const int bb4 = lds_layout(dscene, kLdsStack, 4, 2, &b);
-        if (b16 > 0 && bb4 > 0 && b16 + bb4 <= 160 * 1024) {
+        if (b16 > 0 && bb4 > 0 && lds_alloc(b16) + lds_alloc(bb4) <= kLdsPerCu) {
           dj = a;
           lds_bytes = b16;
           j4 = b;
@@ -1105,6 +1114,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
             "hipMemsetAsync(partial sums)");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
   if (skip_kernel || variant != 3) lds4 = -1;
+  if (const char* e = std::getenv("RTG_LDS4_PAD"); e && lds4 > 0) lds4 += std::atoi(e);  // LDS-granule probe
   if (std::getenv("RTG_VERBOSE"))
     std::fprintf(stderr, "[rtg] schedule %d: %d workgroups of %d waves, %d B LDS, stack %d x %d B, dual %s (%d B)\n",
                  variant, grid_blocks, dj.lds_waves, lds_bytes, stack_depth, dj.stack_esz, lds4 > 0 ? "on" : "off",

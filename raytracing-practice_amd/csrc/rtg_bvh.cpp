@@ -8,7 +8,8 @@
 // The tree is emitted in child-pair form: every node stores both children's boxes, so the
 // traversal tests the two boxes the reference's left->hit / right->hit would test.
 //
-// RTG_BVH_SAH is this library's own binned-SAH builder (16 bins on centroids, leaves <= 4).
+// RTG_BVH_SAH is this library's own binned-SAH builder (32 centroid bins on each of the three axes,
+// leaves <= 4).
 #include <array>
 #include <algorithm>
 #include <cmath>
@@ -148,7 +149,11 @@ struct Builder {
   }
 
   // ---- binned SAH ----
-  static constexpr int kBins = 16;
+  static constexpr int kMaxBins = 64;
+  // 32 bins on all three axes (round 2; round 1: 16 on the longest centroid axis): book-1 -2.3 %,
+  // Cornell -5 %, config 5 -0.5 %, +1.5 s of host build for 1M spheres
+  int kBins = 32;          // centroid bins per axis
+  int axes = 3;            // 1: the centroid box's longest axis only, 3: the best split over all three
   int kMaxLeaf = 4;        // primitives per leaf (<= 8, the leaf code's count field)
   double trav_cost = 0.5;  // cost of one more level relative to one primitive test (measured best)
 
@@ -169,46 +174,49 @@ struct Builder {
         cb.hi[k] = std::max(cb.hi[k], c);
       }
     }
-    const int axis = longest_axis(cb);
-    const double extent = cb.hi[axis] - cb.lo[axis];
+    const int long_axis = longest_axis(cb);
+    int axis = long_axis;
     const double leaf_cost = static_cast<double>(n) * half_area(bbox);
-    if (extent > 0.0) {
-      Box bin_box[kBins];
-      int64_t bin_n[kBins] = {0};
-      const double k1 = kBins * (1.0 - 1e-9) / extent;
-      auto bin_of = [&](int64_t id) {
-        const Box& b = boxes[id];
-        const double c = 0.5 * (b.lo[axis] + b.hi[axis]);
-        int bi = static_cast<int>((c - cb.lo[axis]) * k1);
-        return std::min(std::max(bi, 0), kBins - 1);
-      };
-      for (int64_t i = start; i < end; ++i) {
-        const int bi = bin_of(ids[i]);
-        bin_n[bi]++;
-        bin_box[bi] = box_union(bin_box[bi], boxes[ids[i]]);
-      }
-      double right_area[kBins];
-      int64_t right_n[kBins];
-      Box acc;
-      int64_t accn = 0;
-      for (int b = kBins - 1; b > 0; --b) {
-        acc = box_union(acc, bin_box[b]);
-        accn += bin_n[b];
-        right_area[b] = half_area(acc);
-        right_n[b] = accn;
-      }
+    if (cb.hi[long_axis] - cb.lo[long_axis] > 0.0) {
+      // binned SAH over the longest centroid axis (or all three): the best bin boundary
       double best = kInf;
-      int best_split = -1;
-      Box lacc;
-      int64_t lacc_n = 0;
-      for (int b = 1; b < kBins; ++b) {
-        lacc = box_union(lacc, bin_box[b - 1]);
-        lacc_n += bin_n[b - 1];
-        if (lacc_n == 0 || right_n[b] == 0) continue;
-        const double cost = half_area(lacc) * lacc_n + right_area[b] * right_n[b];
-        if (cost < best) {
-          best = cost;
-          best_split = b;
+      int best_split = -1, best_axis = long_axis;
+      for (int ai = 0; ai < (axes == 3 ? 3 : 1); ++ai) {
+        const int ax = axes == 3 ? ai : long_axis;
+        const double extent = cb.hi[ax] - cb.lo[ax];
+        if (!(extent > 0.0)) continue;
+        Box bin_box[kMaxBins];
+        int64_t bin_n[kMaxBins] = {0};
+        const double k1 = kBins * (1.0 - 1e-9) / extent;
+        for (int64_t i = start; i < end; ++i) {
+          const Box& b = boxes[ids[i]];
+          int bi = static_cast<int>((0.5 * (b.lo[ax] + b.hi[ax]) - cb.lo[ax]) * k1);
+          bi = std::min(std::max(bi, 0), kBins - 1);
+          bin_n[bi]++;
+          bin_box[bi] = box_union(bin_box[bi], b);
+        }
+        double right_area[kMaxBins];
+        int64_t right_n[kMaxBins];
+        Box acc;
+        int64_t accn = 0;
+        for (int b = kBins - 1; b > 0; --b) {
+          acc = box_union(acc, bin_box[b]);
+          accn += bin_n[b];
+          right_area[b] = half_area(acc);
+          right_n[b] = accn;
+        }
+        Box lacc;
+        int64_t lacc_n = 0;
+        for (int b = 1; b < kBins; ++b) {
+          lacc = box_union(lacc, bin_box[b - 1]);
+          lacc_n += bin_n[b - 1];
+          if (lacc_n == 0 || right_n[b] == 0) continue;
+          const double cost = half_area(lacc) * lacc_n + right_area[b] * right_n[b];
+          if (cost < best) {
+            best = cost;
+            best_split = b;
+            best_axis = ax;
+          }
         }
       }
       const double trav = trav_cost * half_area(bbox);
@@ -217,8 +225,13 @@ struct Builder {
         return leaf(start, n);
       }
       if (best_split > 0) {
-        auto it = std::partition(ids.begin() + start, ids.begin() + end,
-                                 [&](int64_t id) { return bin_of(id) < best_split; });
+        axis = best_axis;
+        const double k1 = kBins * (1.0 - 1e-9) / (cb.hi[axis] - cb.lo[axis]);
+        auto it = std::partition(ids.begin() + start, ids.begin() + end, [&](int64_t id) {
+          const Box& b = boxes[id];
+          int bi = static_cast<int>((0.5 * (b.lo[axis] + b.hi[axis]) - cb.lo[axis]) * k1);
+          return std::min(std::max(bi, 0), kBins - 1) < best_split;
+        });
         mid = it - ids.begin();
       }
     } else if (n <= kMaxLeaf) {
@@ -428,13 +441,15 @@ bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
   out->nodes.reserve(n * 2);
   out->refs.reserve(n);
   Builder b{boxes, *out, ids};
-  // RTG_SAH_TUNE="trav_cost:max_leaf" overrides the SAH constants (tuning experiments only)
+  // RTG_SAH_TUNE="trav_cost:max_leaf[:axes[:bins]]" overrides the SAH constants (tuning experiments only)
   if (const char* tune = std::getenv("RTG_SAH_TUNE")) {
     double ct = 0.0;
-    int ml = 0;
-    if (std::sscanf(tune, "%lf:%d", &ct, &ml) == 2 && ct > 0.0 && ml >= 1 && ml <= 8) {
+    int ml = 0, ax = 3, nb = 32;
+    if (std::sscanf(tune, "%lf:%d:%d:%d", &ct, &ml, &ax, &nb) >= 2 && ct > 0.0 && ml >= 1 && ml <= 8) {
       b.trav_cost = ct;
       b.kMaxLeaf = ml;
+      b.axes = ax == 3 ? 3 : 1;
+      b.kBins = std::min(std::max(nb, 2), int(Builder::kMaxBins));
     }
   }
   if (desc->bvh_mode == RTG_BVH_MEDIAN) {

@@ -45,7 +45,8 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     res = {"config": a.config, "lib": a.lib or "default", "layout": a.layout, "height": H, "width": W, "per_n": {}}
     full_ms = None
-    for n in [int(x) for x in a.ns.split(",")]:
+    ns = [int(x) for x in a.ns.split(",")]
+    for n in ([1] if 1 not in ns else []) + sorted(ns, key=lambda x: x != 1):  # N = 1 first: the baseline
         out = torch.zeros((rtgpu.padded_rows(H, n), W, 3), device="cuda")
         kern, wall = [], []
         for r in range(n):
@@ -53,6 +54,10 @@ def main():
             if a.layout == "contig":
                 rows = rtgpu.padded_rows(H, n)
                 b, stride, cnt = r * rows, 1, max(0, min(rows, H - r * rows))
+            if cnt <= 0:  # a rank past the image's last row renders nothing (its shard stays padding)
+                kern.append(0.0)
+                wall.append(0.0)
+                continue
             best_k, best_w = 1e30, 1e30
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -63,11 +68,11 @@ def main():
                 best_k = min(best_k, st.kernel_ms)
             kern.append(round(best_k, 3))
             wall.append(round(best_w, 3))
-        if full_ms is None:
+        if n == 1:  # the efficiency baseline is the one-rank frame, whatever order --ns lists
             full_ms = max(wall)
         res["per_n"][n] = {"kernel_ms": kern, "sum_kernel_ms": round(sum(kern), 3), "wall_ms": wall,
                            "max_wall_ms": max(wall),
-                           "efficiency_vs_n1": round(full_ms / (n * max(wall)), 4)}
+                           "efficiency_vs_n1": (round(full_ms / (n * max(wall)), 4) if full_ms else None)}
         print(json.dumps({n: res["per_n"][n]}), file=sys.stderr, flush=True)
     ds.close()
     print(json.dumps(res))

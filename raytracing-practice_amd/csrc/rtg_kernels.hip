@@ -236,6 +236,8 @@ struct Trav {
   int32_t todo;   // inner node (>= 0: index, or byte offset in 4-wide trees) or leaf code (< 0)
   int32_t sp;     // stack depth
   int32_t origin; // primitive ref the ray starts on (-1: camera ray), DESIGN.md §4 "origin rule"
+  int32_t mat;    // material of the closest hit: the cache-read schedules' shading then fetches the
+                  // material beside the primitive instead of after it (one memory round trip less)
 };
 
 // todo of a finished traversal. "Traversal active" is this integer compare, not a bool of its own:
@@ -521,7 +523,7 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
 
 // Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
 // LDS schedule outside the COUNT diagnostics, as for node codes).
-template <class Stk, bool COUNT, bool CHECK = true>
+template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
   const int32_t code = ~t.todo;
@@ -540,6 +542,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       if (th > 0.0f) {
         t.tbest = th;
         t.best = first + k;
+        if (MAT) t.mat = ibits(sp4[1].w);
       }
     }
     trav_pop(t, stk);
@@ -549,16 +552,20 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     const int32_t ref = S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit);
     float th;
     if (COUNT) cnt.prim += 1;
+    int32_t m = 0;
     if (ref & kQuadRefBit) {  // planar: a ray leaving a quad never hits it again
-      th = ref == t.origin ? -1.0f
-                           : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, t.tbest);
+      const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
+      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest);
+      if (MAT && th > 0.0f) m = ibits(q[1].w);
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
+      if (MAT) m = ibits(sp4[1].w);
     }
     if (th > 0.0f) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
       t.best = ref;
+      if (MAT) t.mat = m;
     }
   }
   trav_pop(t, stk);
@@ -807,8 +814,10 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
 
 // Shades the closest hit `ref` at distance t; returns false when the path ends
 // (ray_color's emission-only return, camera.hpp:213-216, or a miss handled by the caller).
-template <bool FULL>
-__device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
+// MAT: `mat` is the hit's material (Trav::mat), so its record is fetched beside the primitive's
+// (the cache-read schedules: two independent loads instead of a dependent pair)
+template <bool FULL, bool MAT = false>
+__device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, int32_t mat_hit = 0) {
   V3 p, outward;
   float u = 0.0f, v = 0.0f;
   int mat;
@@ -819,7 +828,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
     const V3 C = madd(ps.time, xyz(s1), xyz(s0));
     p = madd(t, ps.d, ps.o);
     outward = scl(div_rn(1.0f, s0.w), sub(p, C));
-    mat = ibits(s1.w);
+    mat = MAT ? mat_hit : ibits(s1.w);
   } else {
     const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
     const float4 q0 = q[0];
@@ -829,7 +838,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t) {
     u = dot(w, cross(hp, xyz(q[2])));
     v = dot(w, cross(xyz(q[1]), hp));
     outward = xyz(q[4]);
-    mat = ibits(q[1].w);
+    mat = MAT ? mat_hit : ibits(q[1].w);
   }
   const bool front = dot(ps.d, outward) < 0.0f;  // set_face_normal, hittable.hpp:29-35
   const V3 n = front ? outward : neg(outward);
@@ -1100,6 +1109,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         if (th > 0.0f) {
           tr.tbest = th;
           tr.best = S.occluder;
+          if (GEOM != kGeomLds) tr.mat = ibits(sp4[1].w);
         }
       }
     }
@@ -1132,7 +1142,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       if (leaf_trip && tr.todo < 0)
-        leaf_step<Stk, COUNT, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
@@ -1168,7 +1178,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         alive_path = false;
       } else {
         if (COUNT) ++w.hits;
-        alive_path = shade<TEXF>(S, ps, tr.best, tr.tbest);
+        alive_path = shade<TEXF, GEOM != kGeomLds>(S, ps, tr.best, tr.tbest, tr.mat);
         if (alive_path && --ps.depth <= 0) alive_path = false;
       }
       uint64_t t_end = 0;

@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "rtg_internal.hpp"
+#include "rtg_numerics.hpp"
 
 
 namespace rtg {
@@ -57,38 +58,7 @@ __device__ __forceinline__ V3 madd(float t, V3 a, V3 b) {  // b + t a
 __device__ __forceinline__ V3 vfma(V3 a, V3 b, V3 c) {  // a * b + c per component
   return v3(fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y), fmaf(a.z, b.z, c.z));
 }
-// Correctly rounded fp32 division and square root without the compiler's special-case steps.
-// div_rn is the IEEE sequence hipcc emits for `x / y` (rcp, two refinements of the reciprocal and
-// of the quotient) minus v_div_scale / v_div_fmas / v_div_fixup, which change nothing unless an
-// operand or the quotient lies within 2^64 of the fp32 range ends (or is 0, inf, NaN): in range
-// the results are the same bits, 8 VALU instead of 11. Every call site divides by a ray length,
-// a radius, a refraction index or a quad denominator (>= 1e-8), and a numerator that is tiny or
-// zero yields a root far below tmin either way.
-__device__ __forceinline__ float div_rn(float x, float y) {
-  const float r0 = __builtin_amdgcn_rcpf(y);
-  const float e0 = fmaf(-y, r0, 1.0f);
-  const float r = fmaf(e0, r0, r0);
-  const float q0 = x * r;
-  const float e1 = fmaf(-y, q0, x);
-  const float q1 = fmaf(e1, r, q0);
-  const float e2 = fmaf(-y, q1, x);
-  return fmaf(e2, r, q1);
-}
-// sqrt_rn: the compiler's correctly rounded sqrt (v_sqrt_f32, then the neighbour whose residual
-// changes sign) without its 2^32 pre-scaling of x < 2^-96 and its 0/inf class fix-up: exact for x
-// == 0 and 2^-96 <= x < inf, 9 VALU instead of 16. Call sites: 1 - z^2 of a 24-bit uniform, a
-// 24-bit uniform, 1 - cos^2 and |1 - |perp|^2| (each 0 or >= 2^-25), and |v|^2 of ray directions
-// (camera rays, and scatter directions kept >= 1e-8 per axis by near_zero). The sphere test's
-// discriminant, which can be arbitrarily small, keeps sqrtf.
-__device__ __forceinline__ float sqrt_rn(float x) {
-  const float s = __builtin_amdgcn_sqrtf(x);
-  const float lo = __int_as_float(__float_as_int(s) - 1);
-  const float hi = __int_as_float(__float_as_int(s) + 1);
-  const float rlo = fmaf(-lo, s, x);
-  const float rhi = fmaf(-hi, s, x);
-  const float t = rlo <= 0.0f ? lo : s;
-  return rhi > 0.0f ? hi : t;
-}
+// div_rn / sqrt_rn: rtg_numerics.hpp (shared with the numerics check, tests/native)
 __device__ __forceinline__ V3 unit(V3 a) {  // unit_vector: v / v.length() == (1/len) * v
   const float len = sqrt_rn(dot(a, a));
   return scl(div_rn(1.0f, len), a);

@@ -718,3 +718,21 @@ def test_comm_world_of_one(gpu_lib, scenes):
     comm2.close()
     comm.close()
     ds.close()
+
+
+def test_numerics_helpers_match_ieee():
+    """div_rn / sqrt_rn (csrc/rtg_numerics.hpp) give the same bits as hipcc's correctly
+    rounded `x / y` and `sqrtf` on 2^24 random operands of each kind from the ranges the kernels use:
+    numerators 2^-60..2^61 (with zeros and ones), divisors 2^-30..2^31, sqrt operands 0 and
+    2^-90..2^101, and the kernels' own sqrt operands (a 24-bit uniform U, 1 - z^2 for z = 1 - 2U,
+    plain and fused)."""
+    import ctypes as C
+    so = C.CDLL(os.path.join(REPO, "tests", "native", "libnumcheck.so"))
+    so.rtg_numerics_check.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_ulonglong), C.POINTER(C.c_float)]
+    so.rtg_numerics_check.restype = C.c_int
+    out, ex = (C.c_ulonglong * 4)(), (C.c_float * 4)()
+    for seed in (0x5EED, 0xC0FFEE):
+        assert so.rtg_numerics_check(1 << 24, seed, out, ex) == 0
+        assert out[3] == 1 << 24
+        assert (out[0], out[1], out[2]) == (0, 0, 0), (list(out), list(ex))
+

@@ -28,6 +28,13 @@ def test_cabi_exports_every_declared_symbol(lib):
     assert lib.lib.rtg_abi_version() == rtgpu.RTG_ABI_VERSION
 
 
+def test_numerics_check_library_loads():
+    """The test library that checks the kernels' div_rn / sqrt_rn against hipcc's IEEE operations
+    (tests/native/numerics_check.hip, run on the GPU by test_gpu.py) is built and exports its entry."""
+    so = C.CDLL(os.path.join(REPO, "tests", "native", "libnumcheck.so"))
+    assert hasattr(so, "rtg_numerics_check")
+
+
 def test_chunk_rule():
     """rtg_chunk_samples (rtgpu.h): one chunk up to 16 spp, chunks of <= 16 samples above."""
     def k(spp):

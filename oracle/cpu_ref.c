@@ -672,7 +672,8 @@ static inline f3 fvfma(f3 a, f3 b, f3 c) { return F3(fmaf(a.x, b.x, c.x), fmaf(a
 static inline f3 funit(f3 a) { return fscl(1.0f / sqrtf(fdot(a, a)), a); }
 static inline f3 fd(const double v[3]) { return F3((float)v[0], (float)v[1], (float)v[2]); }
 
-/* counter RNG: state = mix64(((pixel << 32) | sample) ^ mix64(seed)); PCG32 XSH-RR draws */
+/* counter RNG (DESIGN.md §4 RNG): state = mix64(((pixel << 32) | sample) ^ mix64(seed)); each draw
+   advances the 64-bit LCG (PCG's constants) and takes the top 24 bits of the new state */
 static inline uint64_t mix64(uint64_t z) {
   z ^= z >> 30;
   z *= 0xbf58476d1ce4e5b9ull;
@@ -681,14 +682,10 @@ static inline uint64_t mix64(uint64_t z) {
   z ^= z >> 31;
   return z;
 }
-static inline uint32_t pcg32(uint64_t* s) {
-  uint64_t old = *s;
-  *s = old * 6364136223846793005ull + 1442695040888963407ull;
-  uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-  uint32_t rot = (uint32_t)(old >> 59);
-  return (xs >> rot) | (xs << ((32u - rot) & 31u));
+static inline float U(uint64_t* s) {
+  *s = *s * 6364136223846793005ull + 1442695040888963407ull;
+  return (float)(uint32_t)(*s >> 40) * 5.9604644775390625e-8f;
 }
-static inline float U(uint64_t* s) { return (float)(pcg32(s) >> 8) * 5.9604644775390625e-8f; }
 
 /* exported for KATs */
 uint64_t orc_rng_state(uint64_t seed, uint32_t pixel, uint32_t sample) {

@@ -67,8 +67,11 @@ __device__ __forceinline__ V3 xyz(float4 f) { return v3(f.x, f.y, f.z); }
 __device__ __forceinline__ int ibits(float f) { return __float_as_int(f); }
 
 // ---------------------------------------------------------------------------------------
-// Counter RNG: PCG32 (XSH-RR) seeded per (pixel, sample) by a splitmix64
-// finaliser. Replaces the global glibc rand() stream (rtweekend.hpp:23-39, hazard H1).
+// Counter RNG: a 64-bit LCG (PCG's multiplier and increment) seeded per
+// (pixel, sample) by a splitmix64 finaliser; a draw is the top 24 bits of the advanced state.
+// Replaces the global glibc rand() stream (rtweekend.hpp:23-39, hazard H1). Round 1 drew PCG32
+// XSH-RR outputs; the top bits of the 64-bit state are as good for 24-bit uniforms (G5 tests)
+// at 7 VALU per draw instead of ~14.
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 30;
   z *= 0xbf58476d1ce4e5b9ull;
@@ -77,15 +80,14 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 31;
   return z;
 }
-__device__ __forceinline__ uint32_t pcg_next(uint64_t& s) {
-  const uint64_t old = s;
-  s = old * 6364136223846793005ull + 1442695040888963407ull;
-  const uint32_t xs = static_cast<uint32_t>(((old >> 18) ^ old) >> 27);
-  const uint32_t rot = static_cast<uint32_t>(old >> 59);
-  return (xs >> rot) | (xs << ((32u - rot) & 31u));
-}
 __device__ __forceinline__ float uniform(uint64_t& s) {  // random_double(), [0,1), 24 bits
-  return static_cast<float>(pcg_next(s) >> 8) * 5.9604644775390625e-8f;
+  s = s * 6364136223846793005ull + 1442695040888963407ull;
+  // bits 63..40, converted by an explicit v_cvt_f32_u32: the compiler widens a plain
+  // (float)(uint32_t)(s >> 40) back into a 64-bit integer-to-float expansion (+6 VALU per draw)
+  const uint32_t top = static_cast<uint32_t>(s >> 32) >> 8;
+  float f;
+  asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(top));
+  return f * 5.9604644775390625e-8f;
 }
 
 // sin and cos of 2*pi*u, u in [0,1): quadrant reduction and Taylor polynomials on [-pi/4, pi/4),

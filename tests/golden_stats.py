@@ -75,7 +75,7 @@ def assert_statistical_parity(frame, m, n_frame, z_max=4.0, frac=0.999, global_s
     dark paths): 4 at GPU sample counts, 5 for the CPU oracle's few samples per pixel.
     At least two blocks may exceed z_max whatever the frame size: at 16 spp a light-lit scene's
     block means are heavy-tailed, and across 40 seeds of the 120x120 Cornell frame (675
-    block-channels each) 9 block-channels exceeded 5 sigma with the PCG32 draws in use (4 with a
+    block-channels each) 9 block-channels exceeded 5 sigma with the round-1 PCG32 draws (4 with a
     multiply-with-carry generator tried in round 2), so a "none of 675" rule (0.999 of 675) failed
     about one seed in ten whatever the generator."""
     z, noisy, gz = block_z(frame, m["mean"], m["var"], n_frame, int(m["n"]))

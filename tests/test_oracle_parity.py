@@ -101,6 +101,32 @@ def test_direct_sampling_is_accurate_and_uniform(oracle):
     assert np.allclose((v ** 2).mean(axis=0), 1.0 / 3.0, atol=0.01)
 
 
+def test_counter_rng_streams_are_uniform_and_independent(oracle):
+    """The counter RNG (a splitmix64-seeded 64-bit LCG per (pixel, sample), top 24 bits
+    per draw): the first eight draws of 8192 (pixel, sample) streams are each uniform (chi-square over
+    64 bins), consecutive draws of a stream — the (z, azimuth) and (radius, angle) pairs of the
+    samplers — are independent (chi-square over 16 x 16 cells), and neighbouring streams (adjacent
+    pixels, the next sample of a pixel) are uncorrelated. Bounds are ~5 sigma of the statistics."""
+    n, k = 8192, 8
+    d = np.array([oracle.rng_uniforms(0x5EED, 1000 + i // 4, i % 4, k) for i in range(n)], dtype=np.float64)
+    assert np.all((d >= 0.0) & (d < 1.0))
+    assert np.all(np.round(d * 2 ** 24) == d * 2 ** 24)  # 24-bit uniforms
+    exp1 = n / 64
+    for j in range(k):
+        h = np.bincount((d[:, j] * 64).astype(int), minlength=64)
+        chi = float(((h - exp1) ** 2 / exp1).sum())
+        assert chi < 63 + 5 * math.sqrt(2 * 63), (j, chi)
+    exp2 = n / 256
+    for j in range(k - 1):
+        cell = (d[:, j] * 16).astype(int) * 16 + (d[:, j + 1] * 16).astype(int)
+        h = np.bincount(cell, minlength=256)
+        chi = float(((h - exp2) ** 2 / exp2).sum())
+        assert chi < 255 + 5 * math.sqrt(2 * 255), (j, chi)
+    for a, b in ((d[:-4, 0], d[4:, 0]), (d[:-1, 0], d[1:, 0]), (d[:, 0], d[:, 1])):
+        r = float(np.corrcoef(a, b)[0, 1])
+        assert abs(r) < 5 / math.sqrt(n), r
+
+
 def test_sphere_t32_grazing_far_spheres(oracle):
     """rtg-f32 sphere test on grazing rays: a 0.2-radius sphere 50-1000 units from the
     ray origin (the 1M-sphere field), the ray passing at r·(1 ± δ), δ ≤ 2e-3. Hit/miss must agree with

@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="wall time the all-cores CPU sample is sized for (the 1-core sample adds ~3-5 s)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core of the host (cgroup quota bound)")
+    ap.add_argument("--parity-seconds", type=float, default=4.0,
+                    help="CPU wall time the per-pixel check of the benchmark frame (rows vs cpu_ref32) is "
+                         "sized for; 0 = off")
     a = ap.parse_args()
     for k, v in CONFIGS[a.config].items():
         if getattr(a, k) is None:
@@ -119,6 +122,51 @@ def _cpu_run(args, scene_desc, cam, procs, spp, row_step):
     c.samples_per_pixel = spp
     sec, segs = Oracle().bench_f64(scene_desc, c, procs, H, row_step=row_step)
     return sec, segs, "port", "cpu_ref64"
+
+
+def parity_rows(H, n):
+    """n rows spread evenly over the frame as (first, step, count): a regular stride, so each CPU
+    worker renders its share with one oracle call (one world build) as rows first + k*step."""
+    n = max(1, min(n, H))
+    step = H // n
+    return (H - 1 - step * (n - 1)) // 2, step, n
+
+
+def cpu_parity(scene_desc, cam, gpu_rows, first, step, seed, threads):
+    """The metric's second half ("per-pixel RMSE vs CPU ref", north_star: < 1e-3 with matched
+    per-pixel seeds): rows first + k*step of the benchmark frame the GPU rendered with `seed`
+    (gpu_rows, host copy, linear fp32) against the oracle's fp32 spec (cpu_ref32) on the same seeds,
+    dealt over `threads` CPU threads (ctypes releases the GIL). A checker of the cpu_baseline leg:
+    nothing of the timed region comes from here."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    from oracle_bind import Oracle
+
+    n = gpu_rows.shape[0]
+    threads = max(1, min(threads, n))
+    orc = Oracle()
+    t0 = time.perf_counter()
+
+    def part(t):  # worker t: rows k = t, t + threads, ...
+        cnt = len(range(t, n, threads))
+        return t, orc.render_f32(scene_desc, cam, seed=seed, row_begin=first + t * step,
+                                 row_stride=step * threads, row_count=cnt)[0]
+
+    ref = np.zeros_like(gpu_rows, dtype=np.float32)
+    with ThreadPoolExecutor(threads) as ex:
+        for t, rows in ex.map(part, range(threads)):
+            ref[t::threads] = rows
+    sec = time.perf_counter() - t0
+    g = gpu_rows.astype(np.float64)
+    err = g - ref.astype(np.float64)
+    rmse = float(np.sqrt(np.mean(err ** 2)))
+    return {"vs": "cpu_ref32 (oracle/cpu_ref.c, the fp32 spec of DESIGN.md section 4), same per-pixel seeds",
+            "rows": n, "row_first": first, "row_step": step, "pixels": int(n * gpu_rows.shape[1]),
+            "seed": seed, "rmse": rmse, "max_abs": float(np.max(np.abs(err))),
+            "identical_frac": round(float(np.mean(np.all(gpu_rows == ref, axis=-1))), 6),
+            "tolerance": 1e-3, "pass": bool(rmse < 1e-3 and np.all(np.isfinite(g))),
+            "cpu_threads": threads, "seconds": round(sec, 3)}
 
 
 def cpu_baseline(args, scene_desc, cam):
@@ -256,6 +304,9 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    # host copy of the last timed frame (seed args.seed + warmup + steps - 1), for the per-pixel check
+    last_frame = (shard[:H].cpu().numpy()
+                  if world == 1 and not args.no_cpu_baseline and args.parity_seconds > 0 else None)
 
     tot = torch.tensor([float(segs)], dtype=torch.float64, device="cuda")
     tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -325,6 +376,14 @@ def main():
             line["speedup_vs_cpu"] = round(line["value"] / cb["value"], 1) if cb["value"] else None
             line["speedup_vs_cpu_one_core"] = (round(line["value"] / cb["one_core"]["value"], 1)
                                                if cb["one_core"]["value"] else None)
+            if last_frame is not None:
+                # rows sized for ~parity_seconds on the cores at the measured one-core rate (the
+                # fp32 spec runs at about the reference's speed), 2..128 rows
+                per_row = W * args.spp * max(line["rays_per_sample"], 1.0)
+                nrows = int(args.parity_seconds * cb["cores"] * cb["one_core"]["value"] * 1e6 / per_row)
+                first, pstep, nrows = parity_rows(H, max(2, min(128, nrows)))
+                line["parity"] = cpu_parity(s.desc, cam, last_frame[first::pstep][:nrows], first, pstep,
+                                            args.seed + args.warmup + args.steps - 1, cb["cores"])
         print(json.dumps(line), flush=True)
     if comm is not None:
         torch.cuda.synchronize()

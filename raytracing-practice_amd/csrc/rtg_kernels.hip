@@ -1226,7 +1226,14 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
 // through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
 template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM>
-__global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
+// WAVES = 4: compiled for 5 waves per SIMD (<= 96 VGPRs) and launched with 4-wave workgroups (small
+// scenes, the dual launch's second workgroup) or 16-wave ones (book-1's main launch): one binary for
+// both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
+// the 104-register 16-wave build (dual -0.25 %, single -0.4 %, frames identical), so
+// the workgroup size is read at run time (kFill, wpb) instead of from WAVES.
+__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
+  const int kFill = WAVES == 4 ? static_cast<int>(blockDim.x) : WAVES * 64;  // threads of the workgroup
+  const int wpb = kFill >> 6;                                                // waves of the workgroup
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // the whole-scene LDS schedule of 4-wide trees without a stack spill and without image / noise
   // textures keeps 16-bit stack entries (the LDS room that lets book-1 run the dual launch; the
@@ -1239,7 +1246,7 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
   if constexpr (GEOM == kGeomTreelet) {
     float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
-    for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += WAVES * 64) l_top[k] = S.nodes[k];
+    for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += kFill) l_top[k] = S.nodes[k];
     __syncthreads();
     DevScene L = S;
     L.treelet_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
@@ -1247,7 +1254,7 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
                     static_cast<uint32_t>(J.lds_nodes);
     WaveStats<COUNT> w;
     if constexpr (SPILL) {
-      const int slot = blockIdx.x * WAVES + wave;
+      const int slot = blockIdx.x * wpb + wave;
       const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                   J.lds_stack, J.lds_stack + J.spill_depth};
       render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet>(L, C, J, stk, w);
@@ -1255,7 +1262,7 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
       render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet>(L, C, J, LdsStack<STACK>{lstk}, w);
     }
     flush_stats<COUNT>(J, w, lane);
-    trace_wave(J, t0, w.pixels, lane, blockIdx.x * WAVES + wave, (blockIdx.x << 8) | wave);
+    trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
     return;
   }
   float4* l_nodes = reinterpret_cast<float4*>(smem + J.lds_nodes);
@@ -1264,12 +1271,12 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   float4* l_quads = reinterpret_cast<float4*>(smem + J.lds_quads);
   float4* l_materials = reinterpret_cast<float4*>(smem + J.lds_materials);
   float4* l_textures = reinterpret_cast<float4*>(smem + J.lds_textures);
-  for (int k = threadIdx.x; k < S.num_materials * 2; k += WAVES * 64) l_materials[k] = S.materials[k];
-  for (int k = threadIdx.x; k < S.num_textures * 2; k += WAVES * 64) l_textures[k] = S.textures[k];
+  for (int k = threadIdx.x; k < S.num_materials * 2; k += kFill) l_materials[k] = S.materials[k];
+  for (int k = threadIdx.x; k < S.num_textures * 2; k += kFill) l_textures[k] = S.textures[k];
   // LDS byte address of the node array (inner-node codes of the LDS copy are rebased onto it)
   const int32_t node_rebase = static_cast<int32_t>(static_cast<uint32_t>(
       reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) unsigned char*)smem))) + J.lds_nodes;
-  for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += WAVES * 64) {
+  for (int64_t k = threadIdx.x; k < S.num_nodes * (WIDE == 4 ? 7 : 4); k += kFill) {
     float4 v = S.nodes[k];
     if (WIDE == 4 && k % 7 == 6) {  // code row: inner-node codes become absolute LDS addresses
       int4 c = *reinterpret_cast<int4*>(&v);
@@ -1283,16 +1290,16 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   }
   // sphere records padded to J.lds_sphere_f4 float4s in LDS (3: 48-B stride, an odd number of 16-B
   // bank slots, so the ds_read_b128 of 16 lanes at different spheres spread over all 16 slots)
-  for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += WAVES * 64)
+  for (int64_t k = threadIdx.x; k < S.num_spheres * 2; k += kFill)
     l_spheres[(k >> 1) * J.lds_sphere_f4 + (k & 1)] = S.spheres[k];
-  for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += WAVES * 64) l_quads[k] = S.quads[k];
+  for (int64_t k = threadIdx.x; k < S.num_quads * 5; k += kFill) l_quads[k] = S.quads[k];
   if (S.ref_mode == 0)
-    for (int64_t k = threadIdx.x; k < S.num_refs; k += WAVES * 64) l_refs[k] = S.refs[k];
+    for (int64_t k = threadIdx.x; k < S.num_refs; k += kFill) l_refs[k] = S.refs[k];
   float4* l_pvec = reinterpret_cast<float4*>(smem + J.lds_perlin_vec);
   int32_t* l_pperm = reinterpret_cast<int32_t*>(smem + J.lds_perlin_perm);
   if (TEXF) {
-    for (int k = threadIdx.x; k < S.num_perlins * 256; k += WAVES * 64) l_pvec[k] = S.perlin_vec[k];
-    for (int k = threadIdx.x; k < S.num_perlins * 768; k += WAVES * 64) l_pperm[k] = S.perlin_perm[k];
+    for (int k = threadIdx.x; k < S.num_perlins * 256; k += kFill) l_pvec[k] = S.perlin_vec[k];
+    for (int k = threadIdx.x; k < S.num_perlins * 768; k += kFill) l_pperm[k] = S.perlin_perm[k];
   }
   __syncthreads();
   DevScene L = S;
@@ -1317,7 +1324,7 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
   }
   WaveStats<COUNT> w;
   if constexpr (SPILL) {
-    const int slot = blockIdx.x * WAVES + wave;
+    const int slot = blockIdx.x * wpb + wave;
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
     render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, stk, w);
@@ -1327,7 +1334,7 @@ __global__ __launch_bounds__(WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_
     render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, LdsStack<STACK>{lstk}, w);
   }
   flush_stats<COUNT>(J, w, lane);
-  trace_wave(J, t0, w.pixels, lane, blockIdx.x * WAVES + wave, (blockIdx.x << 8) | wave);
+  trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
 }
 
 // Schedule 1: each loop trip runs one complete closest-hit query per lane through trav_step, so
@@ -1472,17 +1479,17 @@ constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIM
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int WAVES = kLdsWaves>
 hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
-                      int lds_bytes, int grid_blocks, hipStream_t stream) {
+                      int lds_bytes, int grid_blocks, hipStream_t stream, int threads = WAVES * 64) {
   const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>)
                          : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>);
   hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
   if (e != hipSuccess) return e;
   if (count)
     hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>), dim3(grid_blocks),
-                       dim3(WAVES * 64), lds_bytes, stream, S, C, J);
+                       dim3(threads), lds_bytes, stream, S, C, J);
   else
     hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>), dim3(grid_blocks),
-                       dim3(WAVES * 64), lds_bytes, stream, S, C, J);
+                       dim3(threads), lds_bytes, stream, S, C, J);
   return hipGetLastError();
 }
 
@@ -1528,6 +1535,10 @@ hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J
     if (spill || (WIDE == 4 && !tex && !stk16))
       return tex ? launch_lds<kLdsStack, true, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
                  : launch_lds<kLdsStack, true, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+    // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
+    if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
+      return launch_lds<kLdsStack, false, WIDE, false, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream,
+                                                                    kLdsWaves * 64);
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU (A/B)
       return tex ? launch_lds<kLdsStack, false, WIDE, true, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream)
                  : launch_lds<kLdsStack, false, WIDE, false, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream);
@@ -1646,10 +1657,10 @@ hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J,
   }
 }
 
-// The dual launch (rtg_api.cpp) needs the 16-wave kernel's four waves and the 4-wave kernel's one
-// wave of a SIMD to fit its 512 registers per lane together (allocation granule 8): checked on the
-// compiled kernels, so a later change that grows either one drops the dual launch instead of leaving
-// its second workgroup to run after the first has taken all the work.
+// The dual launch (rtg_api.cpp) needs the 16-wave workgroup's four waves and the 4-wave workgroup's
+// one wave of a SIMD to fit its 512 registers per lane together (allocation granule 8): checked on the
+// compiled kernel, so a later change that grows it drops the dual launch instead of leaving its
+// second workgroup to run after the first has taken all the work.
 bool dual_fits_registers(bool count) {
   auto alloc = [](const void* fn) {
     hipFuncAttributes a{};
@@ -1659,11 +1670,10 @@ bool dual_fits_registers(bool count) {
     if (err != hipSuccess) return 1 << 20;
     return (a.numRegs + 7) / 8 * 8;
   };
-  const void* k16 = count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, kLdsWaves, 4, false, kGeomLds>)
-                          : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, kLdsWaves, 4, false, kGeomLds>);
+  // both workgroups run the 4-wave build (launch_default)
   const void* k4 = count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds>)
                          : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds>);
-  return 4 * alloc(k16) + alloc(k4) <= 512;
+  return 5 * alloc(k4) <= 512;
 }
 
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,

@@ -7,9 +7,17 @@ depth 50, on the MI355X kernels of librtgpu.so.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
 A step renders one full frame: rank r renders rows r, r+N, ... (interleaved tiling) into a
-device buffer and the frame is gathered on rank 0 over RCCL (torch.distributed "nccl"). The scene
-is built and uploaded before timing (reported separately). value = ray segments traced by all
-ranks / max-over-ranks wall time of the K timed steps. Prints ONE JSON line on rank 0.
+device buffer and the frame is gathered on rank 0 over RCCL (torch.distributed "nccl" by default, or
+the C-ABI's rtg_gather_rows with --gather-impl rtg). The scene is built and uploaded before timing
+(reported separately as setup_ms). value = ray segments traced by all ranks / max-over-ranks wall
+time of the K timed steps. Prints ONE JSON line on rank 0.
+
+Every line carries the per-pixel check of the benchmark frame itself (`parity`: rows of the last timed
+frame — at N > 1 the frame gathered on rank 0 — against the oracle's fp32 spec on the same seeds).
+N > 1 lines also carry `ranks` (each rank's rows, segments, kernel and gather times, all-gathered
+after timing) and `rtg_gather_check`: after the timed loop, the same shards gathered once more through
+the C-ABI's own RCCL gather (rtg_comm_create_rank, ranks_seen from ncclCommCount) and compared byte for
+byte with the timed frame, under a watchdog, so a fault in that path cannot lose the line.
 """
 import argparse
 import json
@@ -24,6 +32,9 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 
 METRIC = "Mrays/sec at 1920×1080, 500 spp, depth 50; per-pixel RMSE vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# ds_read_b128 / b64 aggregate with every CU streaming at ~2.4 GHz (MI355X_MICROARCH.md §LDS: 256 B/clk/CU)
+LDS_PEAK_GBS = 150000.0
+SIMDS = 1024  # 256 CUs x 4
 BYTES_PER_BOX, BYTES_PER_PRIM, BYTES_PER_HIT = 32, 32, 16  # SURVEY.md §8d algorithmic bytes
 
 
@@ -53,9 +64,15 @@ def parse():
     ap.add_argument("--seed", type=int, default=0x5EED)
     ap.add_argument("--gather", choices=["f32", "rgb8"], default="f32",
                     help="gather the linear fp32 frame (default) or the write_color bytes (4x fewer)")
-    ap.add_argument("--gather-impl", choices=["rtg", "torch"], default="rtg",
-                    help="N>1: the C-ABI's RCCL gather + de-interleave kernel (rtg_gather_rows, default) or "
-                         "torch.distributed.gather + a torch de-interleave")
+    ap.add_argument("--gather-impl", choices=["rtg", "torch"], default="torch",
+                    help="N>1 timed gather: torch.distributed.gather + a torch de-interleave (default until the "
+                         "C-ABI path has run on a multi-GPU node) or the C-ABI's RCCL gather + de-interleave "
+                         "kernel (rtg_gather_rows)")
+    ap.add_argument("--no-rtg-check", action="store_true",
+                    help="N>1: skip the untimed rtg_gather_rows cross-check of the last frame")
+    ap.add_argument("--check-timeout", type=float, default=180.0,
+                    help="N>1: seconds the rtg_gather_rows cross-check may take before the line is printed "
+                         "without it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="wall time the all-cores CPU sample is sized for (the 1-core sample adds ~3-5 s)")
@@ -201,37 +218,73 @@ def cpu_baseline(args, scene_desc, cam):
                          "sample": f"{rows1} rows (every {step1}th), {spp1} spp, 1 process ({what})"}}
 
 
-def pmc_traffic(workload):
-    """HBM bytes per render launch measured by rocprofv3 PMC passes (profiles/pmc_traffic.json,
-    written by tools/pmc_report.py --write-traffic from tools/profile.sh passes of the same workload);
-    None when no matching measurement exists."""
-    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+def _pmc_record(name, workload):
+    """The record of `workload` in profiles/<name> (a {"records": [...]} file written by
+    tools/pmc_report.py from rocprofv3 PMC passes of the same command; an older single-record file is
+    read as one record), or None when that workload was not measured."""
     try:
-        with open(path) as f:
-            rec = json.load(f)
-        if rec.get("workload") == workload:
-            return rec.get("hbm_bytes_per_launch")
+        with open(os.path.join(REPO, "profiles", name)) as f:
+            doc = json.load(f)
     except (OSError, ValueError):
-        pass
-    return None
-
-
-def pmc_binding(workload):
-    """The binding resource of the render kernel for this workload (profiles/pmc_binding.json, written
-    by tools/pmc_report.py --write-binding from rocprofv3 PMC passes of the same command): VALU issue
-    fraction, lane utilisation, wave-cycle split, LDS bank conflicts. None when not measured."""
-    try:
-        with open(os.path.join(REPO, "profiles", "pmc_binding.json")) as f:
-            rec = json.load(f)
+        return None
+    for rec in doc.get("records", [doc]):
         if rec.get("workload") == workload:
             return rec
-    except (OSError, ValueError):
-        pass
     return None
+
+
+def pmc_traffic(workload):
+    """HBM bytes per render launch (FETCH_SIZE x2 + WRITE_SIZE, separate passes, MI355X_MICROARCH.md
+    §HBM), or None."""
+    rec = _pmc_record("pmc_traffic.json", workload)
+    return rec.get("hbm_bytes_per_launch") if rec else None
+
+
+def pmc_binding(workload, kernel_s, plan):
+    """The binding resource of the render kernel for this workload: VALU issue fraction, lane
+    utilisation, wave-cycle split, LDS bank conflicts (profiles/pmc_binding.json), with the register
+    count replaced by the compiled kernel's own (rtg_render_plan) and, where the counters could only
+    see a different launch than the timed one (the dual launch: counter collection serialises its two
+    dispatches), the issue fraction re-derived for the timed launch from the counted instructions."""
+    rec = _pmc_record("pmc_binding.json", workload)
+    if rec is None:
+        return None
+    rec = dict(rec)
+    rec.pop("vgpr", None)  # rocprofv3's VGPR_Count is an allocation-granule field, not the count
+    rec["vgprs"] = plan.get("vgprs")
+    rec["timed_launch"] = {k: plan.get(k) for k in ("schedule", "workgroups", "waves_per_workgroup", "dual",
+                                                     "dual_workgroups", "waves_per_simd", "vgprs", "dual_vgprs")}
+    insts, clk = rec.get("sq_insts_valu_per_launch"), rec.get("effective_clock_ghz")
+    if insts and clk and kernel_s > 0:
+        issue = 2.0 * insts / (SIMDS * kernel_s * clk * 1e9)
+        rec["valu_issue_frac_timed"] = round(issue, 4)
+        if rec.get("valu_lane_utilization"):
+            rec["useful_valu_frac_timed"] = round(issue * rec["valu_lane_utilization"], 4)
+    return rec
+
+
+class _Watchdog:
+    """Runs fn() in this thread; if it has not returned after `seconds`, on_timeout() runs on a timer
+    thread (it prints the line and ends the process: a hang in an optional check must not lose it)."""
+
+    def __init__(self, seconds, on_timeout):
+        import threading
+
+        self.t = threading.Timer(seconds, on_timeout)
+        self.t.daemon = True
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.t.cancel()
+        return False
 
 
 def main():
     args = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -258,10 +311,13 @@ def main():
     t_scene = time.perf_counter() - t0
     params = lib.camera_resolve(cam)
     H, W = params.image_height, params.image_width
+    t1 = time.perf_counter()
     ds = lib.scene_create(s.desc, device=local)
+    t_create = time.perf_counter() - t1
     info = ds.info()
-    b, stride, n = rtgpu.shard_rows(H, rank, world)
-    shard = torch.zeros((rtgpu.padded_rows(H, world), W, 3), dtype=torch.float32, device="cuda")
+    b, stride, n, padded = lib.shard_layout(H, world, rank)
+    plan = ds.plan(cam, row_begin=b, row_stride=stride, row_count=n).as_dict() if n > 0 else {}
+    shard = torch.zeros((padded, W, 3), dtype=torch.float32, device="cuda")
     shard8 = torch.zeros(shard.shape, dtype=torch.uint8, device="cuda") if args.gather == "rgb8" else None
     stream = torch.cuda.current_stream().cuda_stream
     comm, frame = None, None
@@ -273,8 +329,10 @@ def main():
         if rank == 0:
             frame = torch.zeros((H, W, 3), dtype=(torch.uint8 if shard8 is not None else torch.float32),
                                 device="cuda")
+    ev_g0, ev_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gathered = [None]  # the last gathered frame (rank 0, N > 1)
 
-    def step(i):
+    def step(i, evs=None):
         # a rank past the image's last row renders nothing (its shard stays zero padding)
         st = (ds.render_device(cam, shard.data_ptr(), stream, seed=args.seed + i, row_begin=b,
                                row_stride=stride, row_count=n) if n > 0 else rtgpu.rtg_render_stats())
@@ -282,11 +340,15 @@ def main():
             ds.resolve_rgb8(shard.data_ptr(), shard8.data_ptr(), shard.shape[0] * W, stream)
         if world > 1:
             src = shard8 if shard8 is not None else shard
+            g0, g1 = evs if evs is not None else (ev_g0, ev_g1)
+            g0.record()
             if comm is not None:  # ncclGather to rank 0 + the de-interleave kernel there (rtg_gather_rows)
                 comm.gather_rows([src.data_ptr()], H, W * 3 * src.element_size(), 0,
                                  frame.data_ptr() if frame is not None else 0, [stream])
+                gathered[0] = frame
             else:
-                rtgpu.gather_frame(src, H)
+                gathered[0] = rtgpu.gather_frame(src, H)
+            g1.record()
         return st
 
     for i in range(args.warmup):
@@ -296,17 +358,26 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     segs, kernel_ms = 0, []
+    # one event pair per timed step around the gather, on the render stream (torch's current stream)
+    gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if world > 1 else [None] * args.steps
     for i in range(args.steps):
-        st = step(args.warmup + i)
+        st = step(args.warmup + i, gev[i])
         segs += st.segments
         kernel_ms.append(st.kernel_ms)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    gather_ms = [a.elapsed_time(b_) for a, b_ in gev] if world > 1 else []
     # host copy of the last timed frame (seed args.seed + warmup + steps - 1), for the per-pixel check
-    last_frame = (shard[:H].cpu().numpy()
-                  if world == 1 and not args.no_cpu_baseline and args.parity_seconds > 0 else None)
+    want_parity = not args.no_cpu_baseline and args.parity_seconds > 0
+    last_frame = None
+    if want_parity:
+        if world == 1:
+            last_frame = shard[:H].cpu().numpy()
+        elif rank == 0 and gathered[0] is not None:
+            last_frame = gathered[0].cpu().numpy()
 
     tot = torch.tensor([float(segs)], dtype=torch.float64, device="cuda")
     tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
@@ -324,10 +395,29 @@ def main():
     achieved = algo_bytes / avg_kernel_s / 1e9
     workload = (f"{args.scene}(grid={args.grid}) {W}x{H} {args.spp}spp depth{args.depth} bvh={args.bvh} "
                 f"chunk={rtgpu.chunk_samples(args.spp)}")
-    traffic = pmc_traffic(workload)
+    traffic = pmc_traffic(workload) if world == 1 else None
+    setup_ms = {"scene_build_ms": round(t_scene * 1e3, 1), "scene_create_ms": round(t_create * 1e3, 1),
+                "bvh_build_ms": round(info.build_ms, 1), "upload_ms": round(info.upload_ms, 1)}
+    my = {"rank": rank, "device": local, "rows": n, "row_begin": b, "row_stride": stride,
+          "segments": int(segs), "kernel_ms": round(sum(kernel_ms) / len(kernel_ms), 3),
+          "kernel_ms_max": round(max(kernel_ms), 3),
+          "gather_ms": round(sum(gather_ms) / len(gather_ms), 3) if gather_ms else None,
+          "gather_ms_max": round(max(gather_ms), 3) if gather_ms else None,
+          "wall_s": round(dt, 4), "setup_ms": round((t_scene + t_create) * 1e3, 1),
+          "vgprs": plan.get("vgprs"), "schedule": plan.get("schedule")}
+    ranks = [my]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, my)
 
+    line = None
     if rank == 0:
         samples = W * H * args.spp * args.steps
+        lds = {"achieved": round(achieved, 2), "peak": LDS_PEAK_GBS, "unit": "GB/s",
+               "frac": round(achieved / LDS_PEAK_GBS, 4),
+               "note": "the same algorithmic bytes against the ds_read_b128 aggregate (MI355X_MICROARCH.md "
+                       "§LDS): the scene is LDS-resident for configs 2-4 (config 5: the top of the tree)"}
+        binding = pmc_binding(workload, avg_kernel_s, plan) if world == 1 else None
         line = {
             "metric": METRIC,
             "value": round(total_segs / wall / 1e6, 3),
@@ -353,37 +443,76 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_gbs": (round(traffic / avg_kernel_s / 1e9, 2) if traffic else None),
+                         "lds": lds,
+                         "useful_valu_frac": (binding or {}).get("useful_valu_frac_timed",
+                                                                 (binding or {}).get("useful_valu_frac")),
                          "note": ("frac > 1: the algorithmic bytes are served on chip (LDS-resident scene, "
-                                  "or L2/MALL for scenes too large for LDS); traffic = PMC-measured HBM bytes "
-                                  "per launch (null when not measured for this workload); the binding "
-                                  "resource is VALU issue and LDS/cache latency (DESIGN.md section 6)"),
-                         "binding": pmc_binding(workload),
+                                  "or L2/MALL for scenes too large for LDS), so the HBM fraction is not the "
+                                  "bound; `lds.frac` prices the same bytes against the LDS read aggregate and "
+                                  "`useful_valu_frac` is the fraction of the chip's fp32 lane-issue slots doing "
+                                  "path-tracing work in the timed launch (binding: VALU issue x lane "
+                                  "utilisation, DESIGN.md section 6); traffic = PMC-measured HBM bytes per "
+                                  "launch (null when not measured for this workload)"),
+                         "binding": binding,
                          "kernel_ms": round(avg_kernel_s * 1e3, 3),
                          "algorithmic_bytes_per_launch": int(algo_bytes),
                          "per_segment": {"box_tests": round(cst.box_tests / max(cst.segments, 1), 3),
                                          "prim_tests": round(cst.prim_tests / max(cst.segments, 1), 3),
                                          "hit_frac": round(cst.hits / max(cst.segments, 1), 4)}},
+            "launch": plan,
             "msamples_per_s": round(samples / wall / 1e6, 3),
             "rays_per_sample": round(total_segs / samples, 4),
+            "setup_ms": round((t_scene + t_create) * 1e3, 1),
+            "setup": setup_ms,
             "scene_build_ms": round(t_scene * 1e3, 1),
             "bvh": {"nodes": info.num_nodes, "depth": info.bvh_depth, "build_ms": round(info.build_ms, 1),
                     "upload_ms": round(info.upload_ms, 1)},
             "cpu_baseline": None,
         }
+        if world > 1:
+            line["ranks"] = ranks
+            line["gather_ms"] = [r["gather_ms"] for r in ranks]
+            line["kernel_ms_per_rank"] = [r["kernel_ms"] for r in ranks]
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args, s.desc, cam)
             cb = line["cpu_baseline"]
             line["speedup_vs_cpu"] = round(line["value"] / cb["value"], 1) if cb["value"] else None
             line["speedup_vs_cpu_one_core"] = (round(line["value"] / cb["one_core"]["value"], 1)
                                                if cb["one_core"]["value"] else None)
-            if last_frame is not None:
-                # rows sized for ~parity_seconds on the cores at the measured one-core rate (the
-                # fp32 spec runs at about the reference's speed), 2..128 rows
-                per_row = W * args.spp * max(line["rays_per_sample"], 1.0)
-                nrows = int(args.parity_seconds * cb["cores"] * cb["one_core"]["value"] * 1e6 / per_row)
-                first, pstep, nrows = parity_rows(H, max(2, min(128, nrows)))
-                line["parity"] = cpu_parity(s.desc, cam, last_frame[first::pstep][:nrows], first, pstep,
-                                            args.seed + args.warmup + args.steps - 1, cb["cores"])
+        if last_frame is not None:
+            cores = host_cpus()[0]
+            cb = line["cpu_baseline"]
+            # rows sized for ~parity_seconds on the cores at the measured one-core rate (the fp32 spec
+            # runs at about the reference's speed; 2.5 Mrays/s per core assumed
+            # where no CPU baseline was timed, i.e. N > 1), 2..128 rows
+            rate1 = cb["one_core"]["value"] if cb else 2.5
+            per_row = W * args.spp * max(line["rays_per_sample"], 1.0)
+            nrows = int(args.parity_seconds * cores * rate1 * 1e6 / per_row)
+            first, pstep, nrows = parity_rows(H, max(2, min(128, nrows)))
+            rows = last_frame[first::pstep][:nrows]
+            seed_last = args.seed + args.warmup + args.steps - 1
+            if last_frame.dtype == np.uint8:  # --gather rgb8: write_color bytes against the oracle's
+                line["parity"] = cpu_parity_rgb8(s.desc, cam, rows, first, pstep, seed_last, cores)
+            else:
+                line["parity"] = cpu_parity(s.desc, cam, rows, first, pstep, seed_last, cores)
+            if world > 1:
+                line["parity"]["frame"] = f"gathered on rank 0 from {world} ranks"
+
+    if world > 1 and not args.no_rtg_check:
+        # the C-ABI's RCCL gather, untimed, on the last frame's shards: byte-compared with the timed frame
+        def give_up():
+            if rank == 0:
+                line["rtg_gather_check"] = {"status": f"timeout after {args.check_timeout:.0f} s"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        with _Watchdog(args.check_timeout, give_up):
+            line_check = rtg_gather_check(lib, dist, torch, world, rank, local, H, W,
+                                          shard8 if shard8 is not None else shard,
+                                          gathered[0] if rank == 0 else None, stream)
+        if rank == 0:
+            line["rtg_gather_check"] = line_check
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:
         torch.cuda.synchronize()
@@ -391,6 +520,55 @@ def main():
     ds.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def rtg_gather_check(lib, dist, torch, world, rank, local, H, W, src, timed_frame, stream):
+    """One rtg_gather_rows of this rank's last shard (rtg_comm_create_rank; the id broadcast over
+    torch.distributed) into a fresh frame on rank 0, compared byte for byte with the frame the timed
+    loop gathered. Returns the check record on rank 0."""
+    t0 = time.perf_counter()
+    uid = [lib.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = lib.comm_rank(uid[0], world, rank, local)
+    try:
+        ranks_seen = comm.size()[0]
+        out = torch.zeros((H, W, 3), dtype=src.dtype, device="cuda") if rank == 0 else None
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        comm.gather_rows([src.data_ptr()], H, W * 3 * src.element_size(), 0,
+                         out.data_ptr() if out is not None else 0, [stream])
+        e1.record()
+        torch.cuda.synchronize()
+        rec = None
+        if rank == 0:
+            same = bool(torch.equal(out, timed_frame)) if timed_frame is not None else None
+            rec = {"status": "ok", "impl": "rtg_gather_rows (ncclGather + de-interleave kernel)",
+                   "ranks_seen": ranks_seen, "identical_to_timed_frame": same,
+                   "gather_ms": round(e0.elapsed_time(e1), 3),
+                   "seconds_incl_comm_init": round(time.perf_counter() - t0, 3)}
+        dist.barrier()
+        return rec
+    finally:
+        comm.close()
+
+
+def cpu_parity_rgb8(scene_desc, cam, rows8, first, step, seed, threads):
+    """--gather rgb8: the gathered write_color bytes against write_color of the oracle's rows."""
+    import numpy as np
+
+    import rtgpu
+
+    from oracle_bind import Oracle
+
+    orc = Oracle()
+    ref = np.concatenate([orc.render_f32(scene_desc, cam, seed=seed, row_begin=first + k * step, row_stride=step,
+                                         row_count=1)[0] for k in range(rows8.shape[0])])
+    ref8 = rtgpu.write_color_bytes(ref)
+    diff = np.abs(rows8.astype(np.int32) - ref8.astype(np.int32))
+    return {"vs": "write_color(cpu_ref32) bytes", "rows": int(rows8.shape[0]), "row_first": first, "row_step": step,
+            "identical_frac": round(float(np.mean(diff == 0)), 6), "max_abs_lsb": int(diff.max()),
+            "pass": bool(diff.max() <= 1)}
 
 
 if __name__ == "__main__":

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 4
+#define RTG_ABI_VERSION 5
 
 typedef int32_t rtg_status;
 #define RTG_OK 0
@@ -259,6 +259,40 @@ rtg_status rtg_render(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_re
 /* Block until an RTG_RENDER_ASYNC render on `scene` finished; fills the deferred stats. */
 rtg_status rtg_render_wait(rtg_scene* scene, rtg_render_stats* stats);
 
+/* The launch plan rtg_render would use for (scene, cam, job), without rendering (ABI 5): which
+ * kernel schedule, how many persistent workgroups of how many waves, the LDS each one requests,
+ * and the compiled kernel's own resources (hipFuncGetAttributes of the code object that would run:
+ * the real VGPR count, not a profiler's allocation granule). The bench record reports it beside the
+ * roofline so the counted occupancy and the kernel that was timed are named by the library itself. */
+typedef struct rtg_launch_plan {
+  int32_t schedule;          /* 3 LDS-resident scene, 5 LDS treelet, 0 plain grid, 1/2 A/B kernels */
+  int32_t workgroups;        /* main launch */
+  int32_t waves_per_workgroup;
+  int32_t lds_bytes;         /* dynamic LDS per workgroup of the main launch */
+  int32_t vgprs;             /* VGPRs per lane of the main launch's kernel */
+  int32_t sgprs;             /* SGPRs per wave (0 when the runtime does not report it) */
+  int32_t scratch_bytes;     /* private (spill) bytes per lane */
+  int32_t waves_per_simd;    /* resident waves per SIMD of the whole plan (main + dual) */
+  int32_t dual;              /* 1: a second persistent launch of 4-wave workgroups shares the CUs */
+  int32_t dual_workgroups;
+  int32_t dual_lds_bytes;
+  int32_t dual_vgprs;
+  int32_t stack_entry_bytes; /* 2 or 4 */
+  int32_t lds_stack_entries; /* traversal stack entries per lane in LDS (the rest spill to HBM) */
+  int32_t spill_entries;     /* per lane, in the global spill area */
+  int32_t treelet_nodes;     /* schedule 5: 4-wide nodes of the tree's top kept in LDS */
+  int32_t shade_batch;       /* in 64ths of the live lanes */
+  int32_t leaf_batch;        /* lanes */
+  int32_t chunk_samples;     /* K of rtg_chunk_samples */
+  int32_t chunks;
+  int64_t partial_bytes;     /* device scratch of the chunk partial sums this render allocates */
+  int32_t num_cus;
+  int32_t reserved_[7];
+} rtg_launch_plan;
+
+rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,
+                           rtg_launch_plan* out);
+
 /* write_color (color.hpp:26-58) on the device: gamma 2, clamp [0, 0.999], int(256*x).
  * in_rgb / out_rgb8 are device pointers on the scene's device; n_pixels pixels. */
 rtg_status rtg_resolve_rgb8(rtg_scene* scene, const float* in_rgb, uint8_t* out_rgb8,
@@ -280,18 +314,36 @@ rtg_status rtg_comm_create_local(const int32_t* devices, int32_t ndev, rtg_comm*
 rtg_status rtg_comm_unique_id(uint8_t id[RTG_COMM_ID_BYTES]);
 rtg_status rtg_comm_create_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nranks, int32_t rank,
                                 int32_t device, rtg_comm** out);
-/* nranks: ranks of the communicator; nlocal: ranks this process drives. */
+/* nranks: ranks of the communicator as RCCL counts them (ncclCommCount); nlocal: ranks this
+ * process drives. */
 rtg_status rtg_comm_size(const rtg_comm* comm, int32_t* nranks, int32_t* nlocal);
 void rtg_comm_destroy(rtg_comm* comm);
+
+/* Host-only: the interleaved shard of `rank` in an image of `height` rows tiled over `nranks`
+ * (the arithmetic rtg_render_frame and rtg_gather_rows use): rows row_begin + k*row_stride,
+ * k < row_count (0 for a rank past the last row), every shard padded to padded_rows =
+ * ceil(height/nranks) rows, so rank r's block starts at byte r*padded_rows*row_bytes of the root's
+ * staging buffer. Any output pointer may be NULL. */
+rtg_status rtg_shard_layout(int32_t height, int32_t nranks, int32_t rank, int32_t* row_begin,
+                            int32_t* row_stride, int32_t* row_count, int32_t* padded_rows);
 
 /* Gather the interleaved shards of a `height`-row image of `row_bytes`-byte rows onto rank
  * `root`. shards[i] (device memory of the i-th local rank) holds ceil(height/nranks) rows:
  * image rows rank, rank+nranks, ... then padding. out: device memory on root's device, height
  * rows in image order (ignored by processes without the root). streams[i] (hipStream_t, may be
  * NULL = the communicator's own) orders the gather after the render that filled shards[i].
- * Asynchronous: returns once enqueued (every local rank's part, one RCCL group). */
+ * Asynchronous: returns once enqueued (every local rank's part, one RCCL group). The root's staging
+ * buffer is allocated per call on its stream (stream-ordered), so gathers in flight on different
+ * streams do not share it; calls that use a communicator from several host threads at once are
+ * not supported (RCCL groups are per thread). */
 rtg_status rtg_gather_rows(rtg_comm* comm, const void* const* shards, int32_t height, int64_t row_bytes,
                            int32_t root, void* out, void* const* streams);
+
+/* Host twin of the de-interleave step (same index function as the device kernel): `gathered`
+ * holds nranks blocks of ceil(height/nranks) rows in host memory; `out` receives height rows in
+ * image order. For CPU-side gathers (gloo) and for testing the layout without a GPU. */
+rtg_status rtg_deinterleave_rows_host(const void* gathered, void* out, int32_t nranks, int32_t height,
+                                      int64_t row_bytes);
 
 /* The de-interleave step of rtg_gather_rows on its own: `gathered` holds nranks blocks of
  * ceil(height/nranks) rows (block r = rank r's shard); writes image row r + k*nranks from row k of

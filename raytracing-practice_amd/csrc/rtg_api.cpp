@@ -20,11 +20,13 @@ namespace rtg {
 int kernel_stack_depth(int bvh_depth);
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,
                           hipStream_t stream);
-hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
-                         bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream);
+KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool count, int variant);
+hipError_t launch_render(const KernelChoice& k, const DevScene& S, const DevCamera& C, const DevJob& J,
+                         int lds_bytes, int grid_blocks, hipStream_t stream);
+KernelResources kernel_resources(const void* fn);
 int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J);
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J);
-bool dual_fits_registers(bool count);
+bool dual_fits_registers(bool count, bool verbose);
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
 }  // namespace rtg
 
@@ -180,6 +182,33 @@ bool validate_texture(const rtg_scene_desc* d, int32_t tex, int depth, std::stri
 namespace rtg {
 
 rtg_status set_last_error(rtg_status code, const std::string& msg) { return fail(code, msg); }
+
+Knobs read_knobs() {
+  Knobs k;
+  auto num = [](const char* name, int lo, int hi, int* out) {
+    const char* e = std::getenv(name);
+    if (!e || !*e) return false;
+    char* end = nullptr;
+    const long v = std::strtol(e, &end, 10);
+    if (*end != '\0' || v < lo || v > hi) {
+      std::fprintf(stderr, "[rtg] ignoring %s=%s (expected %d..%d)\n", name, e, lo, hi);
+      return false;
+    }
+    *out = static_cast<int>(v);
+    return true;
+  };
+  k.verbose = std::getenv("RTG_VERBOSE") != nullptr;
+  num("RTG_TILE_LW", 0, 6, &k.tile_lw);
+  num("RTG_CHUNK_SAMPLES", 1, 1 << 20, &k.chunk_samples);
+  num("RTG_STACK_LDS_ENTRIES", 1, 32, &k.stack_lds_entries);
+  int w = 0;
+  if (num("RTG_LDS_WAVES", 4, 16, &w) && (w == 4 || w == 16)) k.lds_waves = w;
+  num("RTG_DUAL", 0, 1, &k.dual);
+  int st = 0;
+  if (num("RTG_STACK", 16, 64, &st) && (st == 16 || st == 32 || st == 64)) k.stack = st;
+  if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
+  return k;
+}
 
 void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
   // camera::initialize (camera.hpp:76-136), fp64 with the reference's float-literal quirks.
@@ -586,6 +615,7 @@ struct rtg_scene {
   DevScene dev{};
   rtg_scene_info info{};
   int stack_need = 0;  // structural maximum of traversal stack entries of the BVH
+  Knobs knobs;         // environment knobs, read once when the scene was created
   // host-output renders land in this pinned staging buffer first (DMA to pinned memory completes
   // with the stream; an async copy straight into pageable user memory was seen to return from
   // the stream sync before all of its bytes had arrived), then a host memcpy to the caller
@@ -711,6 +741,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   rtg_scene* s = new (std::nothrow) rtg_scene();
   if (!s) return fail(RTG_E_NOMEM, "host allocation failed");
   s->device = device;
+  s->knobs = read_knobs();
   auto cleanup = [&](rtg_status st) {
     rtg_scene_destroy(s);
     return st;
@@ -870,35 +901,62 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   if (c[4] != 0)
     return fail(RTG_E_UNSUPPORTED, "BVH traversal stack overflow in " + std::to_string(c[4]) + " waves");
   if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
+  if (c[7] != 0)
+    return fail(RTG_E_UNSUPPORTED, "the 16-bit LDS stack layout cannot hold this tree's codes in " +
+                                       std::to_string(c[7]) + " workgroups (nothing rendered)");
   return RTG_OK;
 }
 
-rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,
-                      float* out_rgb, rtg_render_stats* stats) {
+}  // extern "C"
+
+namespace {
+
+// Everything one render decides before it launches (rtg_render executes it, rtg_render_plan
+// reports it): the schedule, the kernels, the LDS layout, the job parameters and the scratch.
+struct Plan {
+  rtg_camera_params cp{};
+  int W = 0, H = 0, rows = 0;
+  bool dev_out = false, async = false, progressive = false, count = false;
+  DevCamera dc{};
+  DevJob dj{};
+  DevJob j4{};  // the dual launch's job (lds4 > 0)
+  DevScene dscene{};
+  int variant = 0;
+  int lds_bytes = -1, lds4 = -1, lds_wgs = 1;
+  int stack_depth = 0, grid_blocks = 1, grid_waves = 0;
+  bool default_sched = false, chunked = false, skip_kernel = false;
+  int sum_chunks = 1;
+  float out_scale = 1.0f;
+  size_t out_bytes = 0;
+  KernelChoice kmain, kaux;
+};
+
+rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, Plan* P) {
   if (!s || !cam || !job) return fail(RTG_E_INVALID, "null argument");
-  const bool progressive = job->partial != nullptr;
-  if (!out_rgb && !progressive) return fail(RTG_E_INVALID, "null output buffer");
+  const Knobs& K = s->knobs;
+  P->progressive = job->partial != nullptr;
   if (cam->image_width <= 0 || cam->samples_per_pixel <= 0)
     return fail(RTG_E_INVALID, "image_width and samples_per_pixel must be positive");
   if (job->row_stride <= 0 || job->row_begin < 0) return fail(RTG_E_INVALID, "bad row range");
-  const bool dev_out = (job->flags & RTG_RENDER_OUT_DEVICE) != 0;
-  const bool async = (job->flags & RTG_RENDER_ASYNC) != 0;
-  if (async && !dev_out) return fail(RTG_E_INVALID, "RTG_RENDER_ASYNC requires RTG_RENDER_OUT_DEVICE");
-  if (s->pending) return fail(RTG_E_INVALID, "a previous async render was not waited for");
+  P->dev_out = (job->flags & RTG_RENDER_OUT_DEVICE) != 0;
+  P->async = (job->flags & RTG_RENDER_ASYNC) != 0;
+  P->count = (job->flags & RTG_RENDER_COUNT) != 0;
+  if (P->async && !P->dev_out) return fail(RTG_E_INVALID, "RTG_RENDER_ASYNC requires RTG_RENDER_OUT_DEVICE");
 
-  rtg_camera_params cp;
-  resolve_camera(cam, &cp);
-  const int W = cp.image_width, H = cp.image_height;
+  resolve_camera(cam, &P->cp);
+  const int W = P->W = P->cp.image_width, H = P->H = P->cp.image_height;
   if (job->row_begin >= H) return fail(RTG_E_INVALID, "row_begin beyond image height");
   const int reachable = (H - 1 - job->row_begin) / job->row_stride + 1;
-  const int rows = job->row_count <= 0 ? reachable : job->row_count;
+  const int rows = P->rows = job->row_count <= 0 ? reachable : job->row_count;
   if (rows > reachable) return fail(RTG_E_INVALID, "row_count reaches past the image");
   if (static_cast<int64_t>(W) * H >= (int64_t(1) << 32))
     return fail(RTG_E_INVALID, "image larger than 2^32 pixels");
   if (W > 65535 || rows > 65535)  // the kernels pack a lane's pixel as 16-bit column / row
     return fail(RTG_E_INVALID, "image width or shard rows above 65535");
+  P->out_bytes = static_cast<size_t>(rows) * W * 3 * sizeof(float);
 
-  DevCamera dc{};
+  DevCamera& dc = P->dc;
+  const rtg_camera_params& cp = P->cp;
   for (int k = 0; k < 3; ++k) {
     dc.center[k] = static_cast<float>(cp.center[k]);
     dc.pixel00[k] = static_cast<float>(cp.pixel00_loc[k]);
@@ -915,22 +973,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   dc.max_depth = cam->max_depth;
   dc.defocus = cam->defocus_angle <= 0.0f ? 0 : 1;  // camera.hpp:155
 
-  RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
-  hipStream_t stream = job->stream ? static_cast<hipStream_t>(job->stream) : s->own_stream;
-  const size_t out_bytes = static_cast<size_t>(rows) * W * 3 * sizeof(float);
-  float* dout = out_rgb;
-  if (!dev_out && out_rgb) {  // a scene-owned device frame (not the stream-ordered pool)
-    if (s->dev_out_bytes < out_bytes) {
-      RTG_HIP(hipStreamSynchronize(stream), "stream sync");
-      if (s->dev_out) RTG_HIP(hipFree(s->dev_out), "hipFree(out)");
-      s->dev_out = nullptr;
-      s->dev_out_bytes = 0;
-      RTG_HIP(hipMalloc(reinterpret_cast<void**>(&s->dev_out), out_bytes), "hipMalloc(out)");
-      s->dev_out_bytes = out_bytes;
-    }
-    dout = s->dev_out;
-  }
-  DevJob dj{};
+  DevJob& dj = P->dj;
+  dj = DevJob{};
   dj.seed_mix = mix64(job->seed);
   dj.row_begin = job->row_begin;
   dj.row_stride = job->row_stride;
@@ -942,11 +986,9 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const int leaf_batch = (job->flags >> 24) & 0x7f;
   const int default_leaf_batch = s->dev.num_nodes <= kSmallBvhNodes ? kSmallBvhLeafBatch : kDefaultLeafBatch;
   dj.leaf_batch = leaf_batch == 0 ? default_leaf_batch : (leaf_batch > 64 ? 64 : leaf_batch);
-  dj.out = dout;
   // tile shape: 8x8 pixels of a contiguous image; wider and flatter tiles for row-interleaved shards,
   // whose consecutive shard rows lie row_stride image rows apart (keeps a wave's rays coherent)
-  dj.tile_lw = job->row_stride <= 1 ? 3 : 4;
-  if (const char* e = std::getenv("RTG_TILE_LW")) dj.tile_lw = std::min(6, std::max(0, std::atoi(e)));
+  dj.tile_lw = K.tile_lw >= 0 ? K.tile_lw : (job->row_stride <= 1 ? 3 : 4);
   {
     const int tw = 1 << dj.tile_lw, th = 64 / tw;
     dj.tiles_x = (W + tw - 1) / tw;
@@ -954,26 +996,26 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   }
   dj.chunk_samples = rtg_chunk_samples(cam->samples_per_pixel);
   // RTG_CHUNK_SAMPLES overrides K for schedule experiments (the frame then differs from the spec)
-  if (const char* e = std::getenv("RTG_CHUNK_SAMPLES")) dj.chunk_samples = std::max(1, std::atoi(e));
+  if (K.chunk_samples > 0) dj.chunk_samples = K.chunk_samples;
   const int total_chunks =
       cam->samples_per_pixel > 0 ? (cam->samples_per_pixel + dj.chunk_samples - 1) / dj.chunk_samples : 1;
   dj.chunks = total_chunks;
   dj.chunk_begin = 0;
   dj.partial = nullptr;
-  int sum_chunks = total_chunks;  // chunks the output mean covers
-  float out_scale = dc.scale;
-  if (progressive) {
+  P->sum_chunks = total_chunks;  // chunks the output mean covers
+  P->out_scale = dc.scale;
+  if (P->progressive) {
     if (job->chunk_begin < 0 || job->chunk_begin >= total_chunks)
       return fail(RTG_E_INVALID, "chunk_begin outside [0, rtg_num_chunks(spp))");
     dj.chunk_begin = job->chunk_begin;
     dj.chunks = job->chunk_count <= 0 ? total_chunks - job->chunk_begin
                                       : std::min(job->chunk_count, total_chunks - job->chunk_begin);
     dj.partial = job->partial;
-    sum_chunks = dj.chunk_begin + dj.chunks;
-    const int samples_done = std::min(cam->samples_per_pixel, sum_chunks * dj.chunk_samples);
+    P->sum_chunks = dj.chunk_begin + dj.chunks;
+    const int samples_done = std::min(cam->samples_per_pixel, P->sum_chunks * dj.chunk_samples);
     // the final mean uses pixel_samples_scale itself (H7), so a finished progressive render is
     // bit-identical to a one-shot one
-    out_scale = sum_chunks == total_chunks ? dc.scale : 1.0f / static_cast<float>(samples_done);
+    P->out_scale = P->sum_chunks == total_chunks ? dc.scale : 1.0f / static_cast<float>(samples_done);
   }
 
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
@@ -982,28 +1024,29 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   // most its occupancy allows), deeper BVHs spill the rest to a global per-wave area; the A/B
   // schedules 1 and 2 keep the whole stack in LDS.
   const int need = std::max(1, s->stack_need);
-  DevScene dscene = s->dev;  // this render's view (the treelet schedule sets its LDS part)
-  dj.lds_sphere_f4 = 3;      // 48-B sphere records in LDS (bank spread)
+  DevScene& dscene = P->dscene;
+  dscene = s->dev;         // this render's view (the treelet schedule sets its LDS part)
+  dj.lds_sphere_f4 = 3;    // 48-B sphere records in LDS (bank spread)
   // persistent LDS schedule, by scene size (DESIGN.md §3 "occupancy"): five 4-wave workgroups per CU
   // when five copies of scene + stacks fit one CU's LDS (5 waves per SIMD at <= 96 VGPRs; Cornell
   // -9.3 %); else one 16-wave workgroup (4 waves per SIMD, the most one workgroup holds) plus, when a
   // second copy fits beside it, a 4-wave workgroup from a second persistent launch (dual, below); else
   // the 16-wave workgroup alone. RTG_LDS_WAVES=16 keeps the single workgroup, RTG_DUAL=0 no dual.
   // stack entries of the persistent LDS schedule: 16-bit for 4-wide trees whose leaf codes fit 16 bits
-  // and whose stack needs no spill (kernel LdsStack16), else 32-bit
-  const char* lds_entries_env = std::getenv("RTG_STACK_LDS_ENTRIES");
+  // (first primitive < 4096) and whose node array ends below 32 KB of LDS (inner codes are absolute LDS
+  // addresses) and whose stack needs no spill (kernel LdsStack16), else 32-bit
+  const bool lds_entries_knob = K.stack_lds_entries > 0;
   const bool stk16 = dscene.node_width == 4 && dscene.num_refs <= 4096 && dscene.num_nodes * 112 <= 32768 &&
-                     need <= kLdsStack && !lds_entries_env && !dscene.tex_full;
+                     need <= kLdsStack && !lds_entries_knob && !dscene.tex_full;
   dj.stack_esz = stk16 ? 2 : 4;
   dj.lds_waves = kLdsWaves;
   int lds_bytes = lds_layout(dscene, kLdsStack, kLdsWaves, dj.stack_esz, &dj);
   int lds_wgs = 1;  // persistent workgroups per CU
   {
-    const char* e = std::getenv("RTG_LDS_WAVES");
     DevJob t = dj;
     const int b4 = lds_layout(dscene, kLdsStack, 4, dj.stack_esz, &t);
-    if ((!e || std::atoi(e) == 4) && dscene.node_width == 4 && need <= kLdsStack && !lds_entries_env && b4 > 0 &&
-        lds_alloc(b4) * kSmallSceneWgs <= kLdsPerCu && (stk16 || dscene.tex_full)) {
+    if ((K.lds_waves == 0 || K.lds_waves == 4) && dscene.node_width == 4 && need <= kLdsStack &&
+        !lds_entries_knob && b4 > 0 && lds_alloc(b4) * kSmallSceneWgs <= kLdsPerCu && (stk16 || dscene.tex_full)) {
       dj = t;
       dj.lds_waves = 4;
       lds_bytes = b4;
@@ -1015,24 +1058,20 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   // copies, with 32-B sphere records if the padded 48-B ones do not fit (book-1: 90 + 66 KB)
   DevJob j4{};
   int lds4 = -1;
-  {
-    const char* e = std::getenv("RTG_DUAL");
-    const char* ew = std::getenv("RTG_LDS_WAVES");
-    if (dj.lds_waves == kLdsWaves && stk16 && !dscene.tex_full && !(e && std::atoi(e) == 0) &&
-        !(ew && std::atoi(ew) == 16) && dual_fits_registers((job->flags & RTG_RENDER_COUNT) != 0)) {
-      for (const int f4 : {3, 2}) {
-        DevJob a = dj, b = dj;
-        a.lds_sphere_f4 = b.lds_sphere_f4 = f4;
-        const int b16 = lds_layout(dscene, kLdsStack, kLdsWaves, 2, &a);
-        const int bb4 = lds_layout(dscene, kLdsStack, 4, 2, &b);
-        if (b16 > 0 && bb4 > 0 && lds_alloc(b16) + lds_alloc(bb4) <= kLdsPerCu) {
-          dj = a;
-          lds_bytes = b16;
-          j4 = b;
-          j4.lds_waves = 4;
-          lds4 = bb4;
-          break;
-        }
+  if (dj.lds_waves == kLdsWaves && stk16 && !dscene.tex_full && K.dual != 0 && K.lds_waves != 16 &&
+      dual_fits_registers(P->count, K.verbose)) {
+    for (const int f4 : {3, 2}) {
+      DevJob a = dj, b = dj;
+      a.lds_sphere_f4 = b.lds_sphere_f4 = f4;
+      const int b16 = lds_layout(dscene, kLdsStack, kLdsWaves, 2, &a);
+      const int bb4 = lds_layout(dscene, kLdsStack, 4, 2, &b);
+      if (b16 > 0 && bb4 > 0 && lds_alloc(b16) + lds_alloc(bb4) <= kLdsPerCu) {
+        dj = a;
+        lds_bytes = b16;
+        j4 = b;
+        j4.lds_waves = 4;
+        lds4 = bb4;
+        break;
       }
     }
   }
@@ -1055,6 +1094,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   if (variant == 3 && lds_bytes < 0) return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
   if ((variant == 1 || variant == 2) && s->dev.node_width != 2)
     return fail(RTG_E_INVALID, "schedules 1 and 2 need a binary BVH (RTG_BVH_MEDIAN)");
+  if (variant < 0 || variant > 5) return fail(RTG_E_INVALID, "unknown render schedule");
   int stack_depth = 0;
   int grid_blocks = 1, grid_waves = 0;
   if (variant == 3 || variant == 5) {
@@ -1069,56 +1109,21 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     stack_depth = kernel_stack_depth(need);
     if (stack_depth < 0) return fail(RTG_E_UNSUPPORTED, "schedules 1 and 2 support BVH stacks up to 64");
   }
-  if (const char* e = std::getenv("RTG_STACK")) stack_depth = std::atoi(e);  // experiments only
+  if (K.stack > 0) stack_depth = K.stack;  // experiments only
   dj.lds_stack = stack_depth;
   // RTG_STACK_LDS_ENTRIES (tests): keep fewer entries in LDS so the global spill path is exercised
-  if (const char* e = lds_entries_env)
-    dj.lds_stack = std::min(stack_depth, std::max(1, std::atoi(e)));
-  const bool default_sched = variant == 3 || variant == 0 || variant == 5;  // the ballot-batched stream
-  dj.spill_depth = default_sched ? std::max(0, need - dj.lds_stack) : 0;
-  dj.spill = nullptr;
-  StreamScratch scratch;
-  scratch.stream = stream;
-  if (dj.spill_depth > 0)
-    RTG_HIP(hipMallocAsync(scratch.add(),
-                           static_cast<size_t>(grid_waves) * 64 * dj.spill_depth * sizeof(int32_t), stream),
-            "hipMallocAsync(stack spill)");
-  if (dj.spill_depth > 0) dj.spill = static_cast<int32_t*>(scratch.ptr[scratch.n - 1]);
-  dj.counters = s->counters;
-  RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
-  // optional per-wave timeline for schedule analysis (tools/wave_trace.py)
-  const char* trace_path = std::getenv("RTG_WAVE_TRACE");
-  int64_t trace_slots = 0;
-  if (trace_path) {
-    trace_slots = default_sched ? int64_t(grid_waves)
-                                               : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
-    RTG_HIP(hipMallocAsync(scratch.add(), trace_slots * 32, stream), "hipMalloc(trace)");
-    dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
-    RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
-  }
-  if (progressive && !default_sched)
+  if (lds_entries_knob) dj.lds_stack = std::min(stack_depth, K.stack_lds_entries);
+  P->default_sched = variant == 3 || variant == 0 || variant == 5;  // the ballot-batched stream
+  dj.spill_depth = P->default_sched ? std::max(0, need - dj.lds_stack) : 0;
+  if (P->progressive && !P->default_sched)
     return fail(RTG_E_INVALID, "progressive rendering needs the default schedules");
-  const bool chunked = !progressive && dj.chunks > 1 && default_sched && dc.max_depth > 0;
-  if (chunked) {
-    RTG_HIP(hipMallocAsync(scratch.add(), out_bytes * dj.chunks, stream), "hipMallocAsync(partial sums)");
-    dj.partial = static_cast<float*>(scratch.ptr[scratch.n - 1]);
-  }
-  if (!default_sched) {  // schedules 1 and 2 keep one running sum per pixel
+  P->chunked = !P->progressive && dj.chunks > 1 && P->default_sched && dc.max_depth > 0;
+  if (!P->default_sched) {  // schedules 1 and 2 keep one running sum per pixel
     dj.chunks = 1;
     dj.chunk_samples = std::max(1, cam->samples_per_pixel);
   }
-  const bool skip_kernel = progressive && dc.max_depth <= 0;  // every chunk sum is black
-  if (skip_kernel)
-    RTG_HIP(hipMemsetAsync(dj.partial + static_cast<size_t>(dj.chunk_begin) * rows * W * 3, 0,
-                           out_bytes * dj.chunks, stream),
-            "hipMemsetAsync(partial sums)");
-  RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
-  if (skip_kernel || variant != 3) lds4 = -1;
-  if (const char* e = std::getenv("RTG_LDS4_PAD"); e && lds4 > 0) lds4 += std::atoi(e);  // LDS-granule probe
-  if (std::getenv("RTG_VERBOSE"))
-    std::fprintf(stderr, "[rtg] schedule %d: %d workgroups of %d waves, %d B LDS, stack %d x %d B, dual %s (%d B)\n",
-                 variant, grid_blocks, dj.lds_waves, lds_bytes, stack_depth, dj.stack_esz, lds4 > 0 ? "on" : "off",
-                 lds4);
+  P->skip_kernel = P->progressive && dc.max_depth <= 0;  // every chunk sum is black
+  if (P->skip_kernel || variant != 3) lds4 = -1;
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
                           j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks};
@@ -1129,7 +1134,133 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     j4.lds_stacks = l4[8];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
+  P->j4 = j4;
+  P->variant = variant;
+  P->lds_bytes = lds_bytes;
+  P->lds4 = lds4;
+  P->lds_wgs = lds_wgs;
+  P->stack_depth = stack_depth;
+  P->grid_blocks = grid_blocks;
+  P->grid_waves = grid_waves;
+  P->kmain = choose_kernel(dscene, dj, stack_depth, P->count, variant);
+  if (!P->skip_kernel && !P->kmain.fn) return fail(RTG_E_INVALID, "no render kernel fits this plan");
   if (lds4 > 0) {
+    P->kaux = choose_kernel(dscene, P->j4, stack_depth, P->count, variant);
+    if (!P->kaux.fn) return fail(RTG_E_INVALID, "no render kernel fits the dual launch");
+  }
+  return RTG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,
+                           rtg_launch_plan* out) {
+  if (!out) return fail(RTG_E_INVALID, "null argument");
+  Plan P;
+  const rtg_status st = plan_render(s, cam, job, &P);
+  if (st != RTG_OK) return st;
+  *out = rtg_launch_plan{};
+  out->schedule = P.variant;
+  out->workgroups = P.variant == 1 || P.variant == 2 ? ((P.W + 15) / 16) * ((P.rows + 15) / 16) : P.grid_blocks;
+  out->waves_per_workgroup = P.kmain.block / 64;
+  out->lds_bytes = P.kmain.dynamic_lds ? P.lds_bytes : 0;
+  const KernelResources r = kernel_resources(P.kmain.fn);
+  out->vgprs = r.vgprs;
+  out->scratch_bytes = r.scratch;
+  out->dual = P.lds4 > 0 ? 1 : 0;
+  int waves_cu = 0;  // resident waves per CU of the persistent schedules
+  if (P.variant == 3) waves_cu = P.lds_wgs * P.dj.lds_waves;
+  if (P.variant == 5) waves_cu = kLdsWaves;
+  if (out->dual) {
+    out->dual_workgroups = s->num_cus;
+    out->dual_lds_bytes = P.lds4;
+    out->dual_vgprs = kernel_resources(P.kaux.fn).vgprs;
+    waves_cu += 4;
+  }
+  out->waves_per_simd = waves_cu / 4;
+  out->stack_entry_bytes = P.dj.stack_esz;
+  out->lds_stack_entries = P.dj.lds_stack;
+  out->spill_entries = P.dj.spill_depth;
+  out->treelet_nodes = P.variant == 5 ? P.dscene.treelet_bytes / 112 : 0;
+  out->shade_batch = P.dj.shade_batch;
+  out->leaf_batch = P.dj.leaf_batch;
+  out->chunk_samples = P.dj.chunk_samples;
+  out->chunks = P.dj.chunks;
+  out->partial_bytes = P.chunked ? static_cast<int64_t>(P.out_bytes) * P.dj.chunks : 0;
+  out->num_cus = s->num_cus;
+  return RTG_OK;
+}
+
+rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,
+                      float* out_rgb, rtg_render_stats* stats) {
+  if (!s || !cam || !job) return fail(RTG_E_INVALID, "null argument");
+  if (!out_rgb && !job->partial) return fail(RTG_E_INVALID, "null output buffer");
+  if (s->pending) return fail(RTG_E_INVALID, "a previous async render was not waited for");
+  Plan P;
+  rtg_status pst = plan_render(s, cam, job, &P);
+  if (pst != RTG_OK) return pst;
+  const Knobs& K = s->knobs;
+  const int W = P.W, rows = P.rows;
+  DevJob& dj = P.dj;
+  DevJob& j4 = P.j4;
+
+  RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+  hipStream_t stream = job->stream ? static_cast<hipStream_t>(job->stream) : s->own_stream;
+  const size_t out_bytes = P.out_bytes;
+  float* dout = out_rgb;
+  if (!P.dev_out && out_rgb) {  // a scene-owned device frame (not the stream-ordered pool)
+    if (s->dev_out_bytes < out_bytes) {
+      RTG_HIP(hipStreamSynchronize(stream), "stream sync");
+      if (s->dev_out) RTG_HIP(hipFree(s->dev_out), "hipFree(out)");
+      s->dev_out = nullptr;
+      s->dev_out_bytes = 0;
+      RTG_HIP(hipMalloc(reinterpret_cast<void**>(&s->dev_out), out_bytes), "hipMalloc(out)");
+      s->dev_out_bytes = out_bytes;
+    }
+    dout = s->dev_out;
+  }
+  dj.out = dout;
+  StreamScratch scratch;
+  scratch.stream = stream;
+  dj.spill = nullptr;
+  if (dj.spill_depth > 0) {
+    RTG_HIP(hipMallocAsync(scratch.add(),
+                           static_cast<size_t>(P.grid_waves) * 64 * dj.spill_depth * sizeof(int32_t), stream),
+            "hipMallocAsync(stack spill)");
+    dj.spill = static_cast<int32_t*>(scratch.ptr[scratch.n - 1]);
+  }
+  dj.counters = s->counters;
+  RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
+  // optional per-wave timeline for schedule analysis (tools/wave_trace.py)
+  const bool trace = !K.wave_trace.empty();
+  int64_t trace_slots = 0;
+  if (trace) {
+    trace_slots = P.default_sched ? int64_t(P.grid_waves) : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
+    RTG_HIP(hipMallocAsync(scratch.add(), trace_slots * 32, stream), "hipMalloc(trace)");
+    dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
+    RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
+  }
+  if (P.chunked) {
+    RTG_HIP(hipMallocAsync(scratch.add(), out_bytes * dj.chunks, stream), "hipMallocAsync(partial sums)");
+    dj.partial = static_cast<float*>(scratch.ptr[scratch.n - 1]);
+  }
+  if (P.skip_kernel)
+    RTG_HIP(hipMemsetAsync(dj.partial + static_cast<size_t>(dj.chunk_begin) * rows * W * 3, 0,
+                           out_bytes * dj.chunks, stream),
+            "hipMemsetAsync(partial sums)");
+  RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
+  const int lds4 = P.lds4;
+  if (K.verbose)
+    std::fprintf(stderr, "[rtg] schedule %d: %d workgroups of %d waves, %d B LDS, stack %d x %d B, dual %s (%d B)\n",
+                 P.variant, P.grid_blocks, P.kmain.block / 64, P.lds_bytes, P.stack_depth, dj.stack_esz,
+                 lds4 > 0 ? "on" : "off", lds4);
+  if (lds4 > 0) {
+    j4.out = dj.out;
+    j4.counters = dj.counters;
+    j4.spill = dj.spill;
+    j4.partial = dj.partial;
     // the aux launch must sit in a hardware queue of its own, or it only starts after the main launch
     // has drained (HIP shares its GPU_MAX_HW_QUEUES = 4 queues round-robin among a process's streams:
     // with RCCL or a second library's streams the two launches serialised, +10 %); high-priority
@@ -1144,26 +1275,22 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     RTG_HIP(hipEventRecord(s->ev_fork, stream), "hipEventRecord");
     RTG_HIP(hipStreamWaitEvent(s->aux_stream, s->ev_fork, 0), "hipStreamWaitEvent");
   }
-  if (!skip_kernel)
-    RTG_HIP(launch_render(dscene, dc, dj, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0,
-                          variant, lds_bytes, grid_blocks, stream),
-            "render kernel launch");
+  if (!P.skip_kernel)
+    RTG_HIP(launch_render(P.kmain, P.dscene, P.dc, dj, P.lds_bytes, P.grid_blocks, stream), "render kernel launch");
   if (lds4 > 0) {
-    RTG_HIP(launch_render(dscene, dc, j4, stack_depth, (job->flags & RTG_RENDER_COUNT) != 0, variant, lds4,
-                          s->num_cus, s->aux_stream),
-            "render kernel launch (aux)");
+    RTG_HIP(launch_render(P.kaux, P.dscene, P.dc, j4, lds4, s->num_cus, s->aux_stream), "render kernel launch (aux)");
     RTG_HIP(hipEventRecord(s->ev_join, s->aux_stream), "hipEventRecord");
     RTG_HIP(hipStreamWaitEvent(stream, s->ev_join, 0), "hipStreamWaitEvent");
   }
-  if (chunked || (progressive && dout))
-    RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, sum_chunks, out_scale, stream),
+  if (P.chunked || (P.progressive && dout))
+    RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, P.sum_chunks, P.out_scale, stream),
             "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");
-  if (trace_path) {
+  if (trace) {
     std::vector<unsigned long long> tr(static_cast<size_t>(trace_slots) * 4);
     RTG_HIP(hipMemcpyAsync(tr.data(), dj.trace, trace_slots * 32, hipMemcpyDeviceToHost, stream), "trace copy");
     RTG_HIP(hipStreamSynchronize(stream), "trace sync");
-    if (FILE* f = std::fopen(trace_path, "wb")) {
+    if (FILE* f = std::fopen(K.wave_trace.c_str(), "wb")) {
       std::fwrite(tr.data(), 8, tr.size(), f);
       std::fclose(f);
     }
@@ -1171,7 +1298,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   RTG_HIP(hipMemcpyAsync(s->host_counters, s->counters, kNumCounters * sizeof(unsigned long long),
                          hipMemcpyDeviceToHost, stream),
           "hipMemcpyAsync(counters)");
-  if (!dev_out && out_rgb) {
+  if (!P.dev_out && out_rgb) {
     if (s->host_stage_bytes < out_bytes) {
       if (s->host_stage) RTG_HIP(hipHostFree(s->host_stage), "hipHostFree(stage)");
       s->host_stage = nullptr;
@@ -1186,12 +1313,12 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   s->pending = true;
   s->pending_stream = stream;
   {
-    const int s0 = std::min(cam->samples_per_pixel, dj.chunk_begin * dj.chunk_samples);
-    const int s1 = progressive ? std::min(cam->samples_per_pixel, (dj.chunk_begin + dj.chunks) * dj.chunk_samples)
-                               : cam->samples_per_pixel;
+    const int spp = cam->samples_per_pixel;
+    const int s0 = std::min(spp, dj.chunk_begin * dj.chunk_samples);
+    const int s1 = P.progressive ? std::min(spp, (dj.chunk_begin + dj.chunks) * dj.chunk_samples) : spp;
     s->pending_samples = static_cast<uint64_t>(rows) * W * static_cast<uint64_t>(s1 - s0);
   }
-  if (async) return RTG_OK;
+  if (P.async) return RTG_OK;
   return collect_stats(s, stats);
 }
 

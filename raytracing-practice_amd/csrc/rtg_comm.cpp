@@ -50,15 +50,14 @@ __global__ __launch_bounds__(256) void deinterleave_kernel(const T* __restrict__
   for (int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; k < total;
        k += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t row = k / row_elems, col = k - row * row_elems;
-    const int64_t r = row % nranks, j = row / nranks;  // image row = r + j*nranks
-    out[k] = gathered[(r * padded + j) * row_elems + col];
+    out[k] = gathered[gathered_row(row, nranks, padded) * row_elems + col];  // image row r + j*nranks
   }
 }
 
 hipError_t launch_deinterleave(const void* gathered, void* out, int32_t nranks, int32_t height, int64_t row_bytes,
                                hipStream_t stream) {
   if (height <= 0 || row_bytes <= 0) return hipSuccess;
-  const int32_t padded = (height + nranks - 1) / nranks;
+  const int32_t padded = shard_layout(height, nranks, 0).padded_rows;
   const bool wide = row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(gathered) % 16 == 0 &&
                     reinterpret_cast<uintptr_t>(out) % 16 == 0;
   const int64_t elems = wide ? row_bytes / 16 : row_bytes;
@@ -81,15 +80,13 @@ struct rtg_comm {
   std::vector<int32_t> ranks, devices;  // per local rank
   std::vector<ncclComm_t> comms;
   std::vector<hipStream_t> streams;     // the communicator's own stream per local rank
-  // scratch, grown on demand: root staging buffer, per-rank shard buffers, root frame
-  void* stage = nullptr;
-  size_t stage_bytes = 0;
+  // scratch, grown on demand: per-rank shard buffers and the root frame of rtg_render_frame (the
+  // gather's staging buffer is allocated per call, stream-ordered, so concurrent gathers never share it)
   std::vector<void*> shard;
   std::vector<size_t> shard_bytes;
   void* frame = nullptr;
   size_t frame_bytes = 0;
   int32_t frame_local = -1;  // local rank whose device holds `frame`
-  int32_t stage_local = -1;
 
   int32_t local_of(int32_t rank) const {
     for (size_t i = 0; i < ranks.size(); ++i)
@@ -195,7 +192,12 @@ rtg_status rtg_comm_create_rank(const uint8_t id[RTG_COMM_ID_BYTES], int32_t nra
 
 rtg_status rtg_comm_size(const rtg_comm* c, int32_t* nranks, int32_t* nlocal) {
   if (!c) return set_last_error(RTG_E_INVALID, "null communicator");
-  if (nranks) *nranks = c->nranks;
+  if (nranks) {  // the rank count as RCCL itself reports it for this communicator
+    int n = 0;
+    if (c->comms.empty() || !c->comms[0]) return set_last_error(RTG_E_INVALID, "communicator not initialised");
+    COMM_NCCL(ncclCommCount(c->comms[0], &n), "ncclCommCount");
+    *nranks = n;
+  }
   if (nlocal) *nlocal = static_cast<int32_t>(c->ranks.size());
   return RTG_OK;
 }
@@ -207,10 +209,6 @@ void rtg_comm_destroy(rtg_comm* c) {
     (void)hipSetDevice(c->devices[i]);
     if (i < c->streams.size() && c->streams[i]) (void)hipStreamSynchronize(c->streams[i]);
     if (i < c->shard.size() && c->shard[i]) (void)hipFree(c->shard[i]);
-  }
-  if (c->stage) {
-    (void)hipSetDevice(c->devices[c->stage_local]);
-    (void)hipFree(c->stage);
   }
   if (c->frame) {
     (void)hipSetDevice(c->devices[c->frame_local]);
@@ -236,11 +234,36 @@ rtg_status rtg_deinterleave_rows(int32_t device, const void* gathered, void* out
   return RTG_OK;
 }
 
+rtg_status rtg_shard_layout(int32_t height, int32_t nranks, int32_t rank, int32_t* row_begin, int32_t* row_stride,
+                            int32_t* row_count, int32_t* padded_rows) {
+  if (height <= 0 || nranks <= 0 || rank < 0 || rank >= nranks)
+    return set_last_error(RTG_E_INVALID, "bad shard layout arguments");
+  const ShardLayout L = shard_layout(height, nranks, rank);
+  if (row_begin) *row_begin = L.row_begin;
+  if (row_stride) *row_stride = L.row_stride;
+  if (row_count) *row_count = L.row_count;
+  if (padded_rows) *padded_rows = L.padded_rows;
+  return RTG_OK;
+}
+
+rtg_status rtg_deinterleave_rows_host(const void* gathered, void* out, int32_t nranks, int32_t height,
+                                      int64_t row_bytes) {
+  if (!gathered || !out || nranks <= 0 || height < 0 || row_bytes < 0)
+    return set_last_error(RTG_E_INVALID, "bad de-interleave arguments");
+  if (height == 0) return RTG_OK;
+  const int32_t padded = shard_layout(height, nranks, 0).padded_rows;
+  const auto* g = static_cast<const uint8_t*>(gathered);
+  auto* o = static_cast<uint8_t*>(out);
+  for (int64_t row = 0; row < height; ++row)
+    std::memcpy(o + row * row_bytes, g + gathered_row(row, nranks, padded) * row_bytes, static_cast<size_t>(row_bytes));
+  return RTG_OK;
+}
+
 rtg_status rtg_gather_rows(rtg_comm* c, const void* const* shards, int32_t height, int64_t row_bytes, int32_t root,
                            void* out, void* const* streams) {
   if (!c || !shards || height <= 0 || row_bytes <= 0 || root < 0 || root >= c->nranks)
     return set_last_error(RTG_E_INVALID, "bad gather arguments");
-  const int32_t N = c->nranks, P = (height + N - 1) / N;
+  const int32_t N = c->nranks, P = shard_layout(height, N, 0).padded_rows;
   const int32_t nlocal = static_cast<int32_t>(c->ranks.size());
   const int32_t rl = c->local_of(root);
   if (rl >= 0 && !out) return set_last_error(RTG_E_INVALID, "null output on the root");
@@ -248,35 +271,49 @@ rtg_status rtg_gather_rows(rtg_comm* c, const void* const* shards, int32_t heigh
   auto stream_of = [&](int32_t i) {
     return (streams && streams[i]) ? static_cast<hipStream_t>(streams[i]) : c->streams[i];
   };
+  // the root's staging buffer: allocated on the root's stream for this call and freed behind the
+  // de-interleave on the same stream (stream-ordered), so two gathers in flight on different streams
+  // (double-buffered frames) each have their own
+  void* stage = nullptr;
   if (rl >= 0) {
-    if (c->stage && c->stage_local != rl) {  // the root moved to another local device
-      (void)hipSetDevice(c->devices[c->stage_local]);
-      COMM_HIP(hipFree(c->stage), "hipFree(stage)");
-      c->stage = nullptr;
-      c->stage_bytes = 0;
-    }
-    c->stage_local = rl;
-    const rtg_status st = ensure(&c->stage, &c->stage_bytes, block * N, c->devices[rl], "hipMalloc(gather stage)");
-    if (st != RTG_OK) return st;
+    COMM_HIP(hipSetDevice(c->devices[rl]), "hipSetDevice");
+    COMM_HIP(hipMallocAsync(&stage, std::max<size_t>(block * N, 16), stream_of(rl)), "hipMallocAsync(gather stage)");
   }
-  COMM_NCCL(ncclGroupStart(), "ncclGroupStart");
+  auto release_stage = [&]() {
+    if (stage) {
+      (void)hipSetDevice(c->devices[rl]);
+      (void)hipFreeAsync(stage, stream_of(rl));  // error path: the enqueue error is what gets reported
+    }
+  };
+  if (const ncclResult_t r = ncclGroupStart(); r != ncclSuccess) {
+    release_stage();
+    return nccl_err(r, "ncclGroupStart");
+  }
   for (int32_t i = 0; i < nlocal; ++i) {
     const hipError_t e = hipSetDevice(c->devices[i]);
     if (e != hipSuccess) {
       (void)ncclGroupEnd();
+      release_stage();
       return hip_err(e, "hipSetDevice");
     }
-    const ncclResult_t r = ncclGather(shards[i], i == rl ? c->stage : nullptr, block, ncclUint8, root, c->comms[i],
+    const ncclResult_t r = ncclGather(shards[i], i == rl ? stage : nullptr, block, ncclUint8, root, c->comms[i],
                                       stream_of(i));
     if (r != ncclSuccess) {
       (void)ncclGroupEnd();
+      release_stage();
       return nccl_err(r, "ncclGather");
     }
   }
-  COMM_NCCL(ncclGroupEnd(), "ncclGroupEnd");
+  if (const ncclResult_t r = ncclGroupEnd(); r != ncclSuccess) {
+    release_stage();
+    return nccl_err(r, "ncclGroupEnd");
+  }
   if (rl >= 0) {
     COMM_HIP(hipSetDevice(c->devices[rl]), "hipSetDevice");
-    COMM_HIP(launch_deinterleave(c->stage, out, N, height, row_bytes, stream_of(rl)), "de-interleave kernel launch");
+    const hipError_t e = launch_deinterleave(stage, out, N, height, row_bytes, stream_of(rl));
+    const hipError_t ef = hipFreeAsync(stage, stream_of(rl));
+    if (e != hipSuccess) return hip_err(e, "de-interleave kernel launch");
+    if (ef != hipSuccess) return hip_err(ef, "hipFreeAsync(gather stage)");
   }
   return RTG_OK;
 }
@@ -288,7 +325,7 @@ rtg_status rtg_render_frame(rtg_comm* c, rtg_scene* const* scenes, const rtg_cam
   rtg_camera_params cp;
   rtg_status st = rtg_camera_resolve(cam, &cp);
   if (st != RTG_OK) return st;
-  const int32_t N = c->nranks, H = cp.image_height, W = cp.image_width, P = (H + N - 1) / N;
+  const int32_t N = c->nranks, H = cp.image_height, W = cp.image_width, P = shard_layout(H, N, 0).padded_rows;
   const int32_t nlocal = static_cast<int32_t>(c->ranks.size());
   const int64_t row_bytes = static_cast<int64_t>(W) * 3 * sizeof(float);
   for (int32_t i = 0; i < nlocal; ++i) {
@@ -315,14 +352,13 @@ rtg_status rtg_render_frame(rtg_comm* c, rtg_scene* const* scenes, const rtg_cam
     }
     shard_ptrs[i] = c->shard[i];
     streams[i] = c->streams[i];
-    const int32_t r = c->ranks[i];
-    const int32_t rows = r < H ? (H - 1 - r) / N + 1 : 0;
-    if (rows == 0) continue;  // a rank past the last row only sends padding
+    const ShardLayout L = shard_layout(H, N, c->ranks[i]);
+    if (L.row_count == 0) continue;  // a rank past the last row only sends padding
     rtg_render_desc job{};
     job.seed = seed;
-    job.row_begin = r;
-    job.row_stride = N;
-    job.row_count = rows;
+    job.row_begin = L.row_begin;
+    job.row_stride = L.row_stride;
+    job.row_count = L.row_count;
     job.flags = RTG_RENDER_OUT_DEVICE | RTG_RENDER_ASYNC;
     job.stream = c->streams[i];
     if ((st = rtg_render(scenes[i], cam, &job, static_cast<float*>(c->shard[i]), nullptr)) != RTG_OK) {

@@ -150,6 +150,19 @@ struct DevScene {
   int32_t sphere_f4;     // float4s per sphere record: 2 in HBM, DevJob::lds_sphere_f4 in the LDS copy
 };
 
+// A render kernel picked for a plan (rtg_kernels.hip choose_kernel); fn == nullptr: none fits.
+struct KernelChoice {
+  const void* fn = nullptr;
+  int block = 0;             // threads per workgroup
+  bool dynamic_lds = false;  // persistent kernels: the plan's LDS bytes are dynamic shared memory
+  bool grid2d = false;       // A/B schedules 1 and 2: one 16x16-pixel workgroup per tile
+};
+struct KernelResources {
+  bool ok = false;
+  int vgprs = 0;
+  int scratch = 0;  // private bytes per lane
+};
+
 struct GpuBvhResult {  // rtg_gpubvh.hip
   int64_t num_nodes;
   int32_t depth;
@@ -160,6 +173,39 @@ hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int3
 
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
 
+// Interleaved row shards of the multi-GPU frame (rtg_shard_layout, rtg_render_frame, rtg_gather_rows):
+// rank r of N renders image rows r, r+N, ...; every shard is padded to P = ceil(H/N) rows.
+struct ShardLayout {
+  int32_t row_begin, row_stride, row_count, padded_rows;
+};
+inline ShardLayout shard_layout(int32_t height, int32_t nranks, int32_t rank) {
+  ShardLayout L;
+  L.row_begin = rank;
+  L.row_stride = nranks;
+  L.row_count = rank < height ? (height - 1 - rank) / nranks + 1 : 0;
+  L.padded_rows = (height + nranks - 1) / nranks;
+  return L;
+}
+// De-interleave: image row `row` comes from row (row / N) of rank (row % N)'s block, i.e. row
+// (row % N) * P + row / N of the gathered staging buffer (shared by the kernel and its host twin).
+__host__ __device__ inline int64_t gathered_row(int64_t row, int32_t nranks, int32_t padded) {
+  return (row % nranks) * padded + row / nranks;
+}
+
+// Tuning / probe knobs of the library, read from the environment once per scene (rtg_scene_create)
+// and clamped there, never per render (a stray variable then cannot change a render mid-run).
+struct Knobs {
+  bool verbose = false;         // RTG_VERBOSE: print the BVH and each render's launch plan
+  int tile_lw = -1;             // RTG_TILE_LW 0..6: log2 tile width (-1: by shard stride)
+  int chunk_samples = 0;        // RTG_CHUNK_SAMPLES >= 1 (schedule experiments; frames leave the spec)
+  int stack_lds_entries = 0;    // RTG_STACK_LDS_ENTRIES 1..32 (tests: exercise the global spill)
+  int lds_waves = 0;            // RTG_LDS_WAVES 4 | 16 (0: by scene size)
+  int dual = -1;                // RTG_DUAL 0 | 1 (-1: where it fits)
+  int stack = 0;                // RTG_STACK 16 | 32 | 64 (A/B schedules only)
+  std::string wave_trace;       // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
+};
+Knobs read_knobs();
+
 struct DevJob {
   uint64_t seed_mix;
   int32_t row_begin;
@@ -168,7 +214,8 @@ struct DevJob {
   int32_t shade_batch;  // schedule 0: shade once ceil(alive * shade_batch / 64) lanes are ready
   float* out;
   // [0] segments, [1] box tests, [2] prim tests, [3] hits, [4] stack overflow, [5] bad BVH code,
-  // [6] persistent kernels' tile counter, [8..23] schedule diagnostics
+  // [6] persistent kernels' tile counter, [7] workgroups that could not run the 16-bit LDS stack
+  // layout (codes past 16 bits: RTG_E_UNSUPPORTED, nothing rendered), [8..23] schedule diagnostics
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 64-pixel tiles per shard row of tiles

@@ -161,7 +161,7 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float q = -(hb + copysignf(sq, hb));
   if (q == 0.0f || a == 0.0f) return -1.0f;
   const float t0 = q * inv_a;
-  const float t1 = div_rn(c, q);
+  const float t1 = div_rn_wide(c, q);  // q has no lower bound (tangent rays): ADVICE r02
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
   if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
@@ -1308,8 +1308,11 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
     L.root_code = node_rebase;
     L.node_limit = node_rebase + static_cast<int32_t>(S.num_nodes) * 112;
   }
-  if (STK16 && L.node_limit > 32768) {  // codes would not fit the 16-bit stack: report, render nothing
-    if (threadIdx.x == 0) atomicAdd(&J.counters[5], 1ull);
+  // 16-bit stack entries hold inner codes (absolute LDS addresses, so the node array must end below
+  // 32 KB of LDS) and leaf codes (first primitive < 4096). The host plans the layout for a dynamic-LDS
+  // base of 0; if that ever changes (e.g. a static __shared__ is added) report, render nothing
+  if (STK16 && (L.node_limit > 32768 || S.num_refs > 4096)) {
+    if (threadIdx.x == 0) atomicAdd(&J.counters[7], 1ull);
     return;
   }
   L.refs = l_refs;
@@ -1478,104 +1481,130 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int WAVES = kLdsWaves>
-hipError_t launch_lds(const DevScene& S, const DevCamera& C, const DevJob& J, bool count,
-                      int lds_bytes, int grid_blocks, hipStream_t stream, int threads = WAVES * 64) {
-  const void* fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>);
-  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
-  if (e != hipSuccess) return e;
-  if (count)
-    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>), dim3(grid_blocks),
-                       dim3(threads), lds_bytes, stream, S, C, J);
-  else
-    hipLaunchKernelGGL((render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>), dim3(grid_blocks),
-                       dim3(threads), lds_bytes, stream, S, C, J);
-  return hipGetLastError();
-}
-
-// Schedule 5: the persistent kernel with an LDS treelet over a scene in HBM (4-wide trees only).
-hipError_t launch_treelet(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int lds_bytes,
-                          int grid_blocks, hipStream_t stream) {
-  if (S.node_width != 4 || J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves)
-    return hipErrorInvalidValue;
-  const bool spill = J.spill_depth > 0, tex = S.tex_full != 0;
-  if (spill)
-    return tex ? launch_lds<kLdsStack, true, 4, true, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream)
-               : launch_lds<kLdsStack, true, 4, false, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream);
-  return tex ? launch_lds<kLdsStack, false, 4, true, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream)
-             : launch_lds<kLdsStack, false, 4, false, kGeomTreelet>(S, C, J, count, lds_bytes, grid_blocks, stream);
+KernelChoice lds_kernel(bool count, int threads = WAVES * 64) {
+  KernelChoice k;
+  k.fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>)
+               : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>);
+  k.block = threads;
+  k.dynamic_lds = true;
+  return k;
 }
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF>
-hipError_t launch_plain(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int grid_blocks,
-                        hipStream_t stream) {
-  if (count)
-    hipLaunchKernelGGL((render_kernel<STACK, SPILL, true, WIDE, TEXF>), dim3(grid_blocks), dim3(256), 0, stream,
-                       S, C, J);
+KernelChoice plain_kernel(bool count) {
+  KernelChoice k;
+  k.fn = count ? reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, true, WIDE, TEXF>)
+               : reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, false, WIDE, TEXF>);
+  k.block = 256;
+  return k;
+}
+
+template <int STACK>
+KernelChoice legacy_kernel(bool count, int variant) {
+  KernelChoice k;
+  if (variant == 2)
+    k.fn = count ? reinterpret_cast<const void*>(&render_kernel_v0<STACK, true>)
+                 : reinterpret_cast<const void*>(&render_kernel_v0<STACK, false>);
   else
-    hipLaunchKernelGGL((render_kernel<STACK, SPILL, false, WIDE, TEXF>), dim3(grid_blocks), dim3(256), 0, stream,
-                       S, C, J);
-  return hipGetLastError();
+    k.fn = count ? reinterpret_cast<const void*>(&render_kernel_segment<STACK, true>)
+                 : reinterpret_cast<const void*>(&render_kernel_segment<STACK, false>);
+  k.block = 256;
+  k.grid2d = true;
+  return k;
+}
+
+// Schedule 5: the persistent kernel with an LDS treelet over a scene in HBM (4-wide trees only).
+KernelChoice treelet_kernel(const DevScene& S, const DevJob& J, bool count) {
+  if (S.node_width != 4 || J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves) return {};
+  const bool spill = J.spill_depth > 0, tex = S.tex_full != 0;
+  if (spill)
+    return tex ? lds_kernel<kLdsStack, true, 4, true, kGeomTreelet>(count)
+               : lds_kernel<kLdsStack, true, 4, false, kGeomTreelet>(count);
+  return tex ? lds_kernel<kLdsStack, false, 4, true, kGeomTreelet>(count)
+             : lds_kernel<kLdsStack, false, 4, false, kGeomTreelet>(count);
 }
 
 // The default schedules: persistent LDS kernel (16 LDS stack entries) or the plain grid (16, or 32
 // with a global spill for deeper trees), each with / without the image-and-noise texture paths.
 template <int WIDE>
-hipError_t launch_default(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int stack,
-                          bool lds, int lds_bytes, int grid_blocks, hipStream_t stream) {
+KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int stack, bool lds) {
   const bool spill = J.spill_depth > 0;
   const bool tex = S.tex_full != 0;
   if (lds) {
-    if (stack != kLdsStack || J.lds_stack > kLdsStack) return hipErrorInvalidValue;
+    if (stack != kLdsStack || J.lds_stack > kLdsStack) return {};
     // 4-wide trees keep 16-bit stack entries (J.stack_esz 2) unless their leaf codes do not fit 16
     // bits (the host then asks for 4-byte entries, which the spill variant holds, with no spill area
     // if none is needed); binary trees keep 32-bit entries
     const bool stk16 = WIDE == 4 && !spill && !tex && J.stack_esz == 2;
-    if (J.stack_esz != (stk16 ? 2 : 4)) return hipErrorInvalidValue;
+    if (J.stack_esz != (stk16 ? 2 : 4)) return {};
     if (spill || (WIDE == 4 && !tex && !stk16))
-      return tex ? launch_lds<kLdsStack, true, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
-                 : launch_lds<kLdsStack, true, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+      return tex ? lds_kernel<kLdsStack, true, WIDE, true>(count) : lds_kernel<kLdsStack, true, WIDE, false>(count);
     // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
     if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
-      return launch_lds<kLdsStack, false, WIDE, false, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream,
-                                                                    kLdsWaves * 64);
-    if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU (A/B)
-      return tex ? launch_lds<kLdsStack, false, WIDE, true, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream)
-                 : launch_lds<kLdsStack, false, WIDE, false, kGeomLds, 4>(S, C, J, count, lds_bytes, grid_blocks, stream);
-    return tex ? launch_lds<kLdsStack, false, WIDE, true>(S, C, J, count, lds_bytes, grid_blocks, stream)
-               : launch_lds<kLdsStack, false, WIDE, false>(S, C, J, count, lds_bytes, grid_blocks, stream);
+      return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, kLdsWaves * 64);
+    if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU; the dual's second launch
+      return tex ? lds_kernel<kLdsStack, false, WIDE, true, kGeomLds, 4>(count)
+                 : lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count);
+    return tex ? lds_kernel<kLdsStack, false, WIDE, true>(count) : lds_kernel<kLdsStack, false, WIDE, false>(count);
   }
-  if (stack > 32 || J.lds_stack > stack) return hipErrorInvalidValue;
+  if (stack > 32 || J.lds_stack > stack) return {};
   if (spill)  // (any LDS part <= 32 entries, J.lds_stack, plus the global spill)
-    return tex ? launch_plain<32, true, WIDE, true>(S, C, J, count, grid_blocks, stream)
-               : launch_plain<32, true, WIDE, false>(S, C, J, count, grid_blocks, stream);
+    return tex ? plain_kernel<32, true, WIDE, true>(count) : plain_kernel<32, true, WIDE, false>(count);
   if (stack == 16)
-    return tex ? launch_plain<16, false, WIDE, true>(S, C, J, count, grid_blocks, stream)
-               : launch_plain<16, false, WIDE, false>(S, C, J, count, grid_blocks, stream);
-  return tex ? launch_plain<32, false, WIDE, true>(S, C, J, count, grid_blocks, stream)
-             : launch_plain<32, false, WIDE, false>(S, C, J, count, grid_blocks, stream);
-}
-
-template <int STACK>
-hipError_t launch_legacy(const DevScene& S, const DevCamera& C, const DevJob& J, bool count, int variant,
-                         hipStream_t stream) {
-  const dim3 block(256);
-  const dim3 grid((C.width + 15) / 16, (J.row_count + 15) / 16);
-  if (variant == 2) {
-    if (count)
-      hipLaunchKernelGGL((render_kernel_v0<STACK, true>), grid, block, 0, stream, S, C, J);
-    else
-      hipLaunchKernelGGL((render_kernel_v0<STACK, false>), grid, block, 0, stream, S, C, J);
-  } else {
-    if (count)
-      hipLaunchKernelGGL((render_kernel_segment<STACK, true>), grid, block, 0, stream, S, C, J);
-    else
-      hipLaunchKernelGGL((render_kernel_segment<STACK, false>), grid, block, 0, stream, S, C, J);
-  }
-  return hipGetLastError();
+    return tex ? plain_kernel<16, false, WIDE, true>(count) : plain_kernel<16, false, WIDE, false>(count);
+  return tex ? plain_kernel<32, false, WIDE, true>(count) : plain_kernel<32, false, WIDE, false>(count);
 }
 
 }  // namespace
+
+// The kernel a render of this plan runs (fn == nullptr: no kernel fits the plan).
+KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool count, int variant) {
+  if (variant == 5) return treelet_kernel(S, J, count);
+  if (variant == 3 || variant == 0)
+    return S.node_width == 4 ? default_kernel<4>(S, J, count, stack, variant == 3)
+                             : default_kernel<2>(S, J, count, stack, variant == 3);
+  // schedules 1 and 2 traverse binary nodes only, without a scene-spanning occluder
+  if (S.node_width != 2 || S.occluder >= 0) return {};
+  switch (stack) {
+    case 16:
+      return legacy_kernel<16>(count, variant);
+    case 32:
+      return legacy_kernel<32>(count, variant);
+    case 64:
+      return legacy_kernel<64>(count, variant);
+    default:
+      return {};
+  }
+}
+
+hipError_t launch_render(const KernelChoice& k, const DevScene& S, const DevCamera& C, const DevJob& J,
+                         int lds_bytes, int grid_blocks, hipStream_t stream) {
+  if (J.row_count <= 0 || C.width <= 0) return hipSuccess;
+  if (!k.fn) return hipErrorInvalidValue;
+  if (k.dynamic_lds) {
+    const hipError_t e = hipFuncSetAttribute(k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  const dim3 grid = k.grid2d ? dim3((C.width + 15) / 16, (J.row_count + 15) / 16) : dim3(grid_blocks);
+  DevScene s = S;
+  DevCamera c = C;
+  DevJob j = J;
+  void* args[] = {&s, &c, &j};
+  return hipLaunchKernel(k.fn, grid, dim3(k.block), args, k.dynamic_lds ? lds_bytes : 0, stream);
+}
+
+// Registers / scratch of a compiled kernel (hipFuncGetAttributes on its code object).
+KernelResources kernel_resources(const void* fn) {
+  KernelResources r;
+  if (!fn) return r;
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, fn) != hipSuccess) return r;
+  r.ok = true;
+  r.vgprs = a.numRegs;
+  r.scratch = static_cast<int>(a.localSizeBytes);
+  return r;
+}
+
 
 int kernel_stack_depth(int bvh_depth) {
   if (bvh_depth <= 16) return 16;
@@ -1636,44 +1665,18 @@ int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
   return static_cast<int>(stacks + nodes * 112);
 }
 
-hipError_t launch_render(const DevScene& S, const DevCamera& C, const DevJob& J, int stack,
-                         bool count, int variant, int lds_bytes, int grid_blocks, hipStream_t stream) {
-  if (J.row_count <= 0 || C.width <= 0) return hipSuccess;
-  if (variant == 5) return launch_treelet(S, C, J, count, lds_bytes, grid_blocks, stream);
-  if (variant == 3 || variant == 0)
-    return S.node_width == 4 ? launch_default<4>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream)
-                             : launch_default<2>(S, C, J, count, stack, variant == 3, lds_bytes, grid_blocks, stream);
-  // schedules 1 and 2 traverse binary nodes only, without a scene-spanning occluder
-  if (S.node_width != 2 || S.occluder >= 0) return hipErrorInvalidValue;
-  switch (stack) {
-    case 16:
-      return launch_legacy<16>(S, C, J, count, variant, stream);
-    case 32:
-      return launch_legacy<32>(S, C, J, count, variant, stream);
-    case 64:
-      return launch_legacy<64>(S, C, J, count, variant, stream);
-    default:
-      return hipErrorInvalidValue;
-  }
-}
-
 // The dual launch (rtg_api.cpp) needs the 16-wave workgroup's four waves and the 4-wave workgroup's
 // one wave of a SIMD to fit its 512 registers per lane together (allocation granule 8): checked on the
 // compiled kernel, so a later change that grows it drops the dual launch instead of leaving its
 // second workgroup to run after the first has taken all the work.
-bool dual_fits_registers(bool count) {
-  auto alloc = [](const void* fn) {
-    hipFuncAttributes a{};
-    const hipError_t err = hipFuncGetAttributes(&a, fn);
-    if (std::getenv("RTG_VERBOSE"))
-      std::fprintf(stderr, "[rtg] dual check: %s numRegs %d\n", hipGetErrorString(err), a.numRegs);
-    if (err != hipSuccess) return 1 << 20;
-    return (a.numRegs + 7) / 8 * 8;
-  };
-  // both workgroups run the 4-wave build (launch_default)
-  const void* k4 = count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds>)
-                         : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds>);
-  return 5 * alloc(k4) <= 512;
+bool dual_fits_registers(bool count, bool verbose) {
+  // both workgroups run the 4-wave build (default_kernel)
+  const KernelResources r = kernel_resources(
+      count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds>)
+            : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds>));
+  if (verbose) std::fprintf(stderr, "[rtg] dual check: numRegs %d\n", r.vgprs);
+  if (!r.ok) return false;
+  return 5 * ((r.vgprs + 7) / 8 * 8) <= 512;
 }
 
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,

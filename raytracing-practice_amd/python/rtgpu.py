@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 
-RTG_ABI_VERSION = 4
+RTG_ABI_VERSION = 5
 RTG_OK = 0
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
 RTG_MAT_LAMBERTIAN, RTG_MAT_METAL, RTG_MAT_DIELECTRIC, RTG_MAT_DIFFUSE_LIGHT = 1, 2, 3, 4
@@ -109,6 +109,17 @@ class rtg_scene_info(C.Structure):
                 ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("upload_ms", C.c_double)]
 
 
+class rtg_launch_plan(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "schedule", "workgroups", "waves_per_workgroup", "lds_bytes", "vgprs", "sgprs", "scratch_bytes",
+        "waves_per_simd", "dual", "dual_workgroups", "dual_lds_bytes", "dual_vgprs", "stack_entry_bytes",
+        "lds_stack_entries", "spill_entries", "treelet_nodes", "shade_batch", "leaf_batch", "chunk_samples",
+        "chunks")] + [("partial_bytes", C.c_int64), ("num_cus", C.c_int32), ("reserved_", C.c_int32 * 7)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved_"}
+
+
 class rtg_bvh_node_host(C.Structure):
     _fields_ = [("lo", (C.c_double * 3) * 2), ("hi", (C.c_double * 3) * 2),
                 ("child", C.c_int32 * 2), ("count", C.c_int32 * 2)]
@@ -125,7 +136,8 @@ RTG_SYMBOLS = ("rtg_abi_version", "rtg_last_error", "rtg_device_count", "rtg_cam
                "rtg_scene_create", "rtg_scene_get_info", "rtg_scene_destroy", "rtg_render",
                "rtg_render_wait", "rtg_resolve_rgb8", "rtg_bvh_build_host", "rtg_comm_create_local",
                "rtg_comm_unique_id", "rtg_comm_create_rank", "rtg_comm_size", "rtg_comm_destroy",
-               "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame")
+               "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame", "rtg_render_plan",
+               "rtg_shard_layout", "rtg_deinterleave_rows_host")
 RTG_COMM_ID_BYTES = 128
 
 
@@ -187,11 +199,14 @@ class Library:
                                             C.c_void_p]
         L.rtg_render_frame.argtypes = [C.c_void_p, _P(C.c_void_p), _P(rtg_camera_desc), C.c_uint64, C.c_int32,
                                        C.c_void_p, _P(rtg_render_stats)]
+        L.rtg_render_plan.argtypes = [C.c_void_p, _P(rtg_camera_desc), _P(rtg_render_desc), _P(rtg_launch_plan)]
+        L.rtg_shard_layout.argtypes = [C.c_int32, C.c_int32, C.c_int32] + [_P(C.c_int32)] * 4
+        L.rtg_deinterleave_rows_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64]
         for name in ("rtg_device_count", "rtg_camera_resolve", "rtg_scene_create",
                      "rtg_scene_get_info", "rtg_render", "rtg_render_wait", "rtg_resolve_rgb8",
                      "rtg_bvh_build_host", "rtg_comm_create_local", "rtg_comm_unique_id",
                      "rtg_comm_create_rank", "rtg_comm_size", "rtg_gather_rows", "rtg_deinterleave_rows",
-                     "rtg_render_frame"):
+                     "rtg_render_frame", "rtg_render_plan", "rtg_shard_layout", "rtg_deinterleave_rows_host"):
             getattr(L, name).restype = C.c_int32
         if L.rtg_abi_version() != RTG_ABI_VERSION:
             raise RuntimeError("librtgpu ABI version mismatch")
@@ -245,6 +260,26 @@ class Library:
         h = C.c_void_p()
         self.check("rtg_comm_create_rank", self.lib.rtg_comm_create_rank(buf, nranks, rank, device, C.byref(h)))
         return Comm(self, h)
+
+    def shard_layout(self, height: int, nranks: int, rank: int):
+        """rtg_shard_layout: (row_begin, row_stride, row_count, padded_rows) of rank's interleaved shard
+        (host only; the arithmetic rtg_render_frame / rtg_gather_rows use)."""
+        v = [C.c_int32(0) for _ in range(4)]
+        self.check("rtg_shard_layout", self.lib.rtg_shard_layout(height, nranks, rank, *[C.byref(x) for x in v]))
+        return tuple(x.value for x in v)
+
+    def deinterleave_rows_host(self, gathered, nranks: int, height: int):
+        """rtg_deinterleave_rows_host on a host array of nranks blocks of padded rows (row = last axes):
+        returns the (height, ...) image in row order (same index function as the device kernel)."""
+        import numpy as np
+
+        g = np.ascontiguousarray(gathered)
+        padded = (height + nranks - 1) // nranks
+        rows = g.reshape(nranks * padded, -1)
+        out = np.empty((height,) + g.shape[1:], dtype=g.dtype)
+        self.check("rtg_deinterleave_rows_host", self.lib.rtg_deinterleave_rows_host(
+            g.ctypes.data, out.ctypes.data, nranks, height, rows.shape[1] * g.itemsize))
+        return out
 
     def deinterleave_rows(self, device: int, gathered_ptr: int, out_ptr: int, nranks: int, height: int,
                           row_bytes: int, stream_ptr: Optional[int] = None) -> None:
@@ -323,6 +358,16 @@ class DeviceScene:
             self.close()
         except Exception:
             pass
+
+    def plan(self, cam: rtg_camera_desc, row_begin: int = 0, row_stride: int = 1, row_count: int = 0,
+             flags: int = RTG_RENDER_OUT_DEVICE) -> rtg_launch_plan:
+        """rtg_render_plan: the launch plan (schedule, workgroups, LDS, the kernel's own VGPR count)
+        a render of these rows would use, without rendering."""
+        job = rtg_render_desc(DEFAULT_SEED, row_begin, row_stride, row_count, flags, None)
+        out = rtg_launch_plan()
+        self.L.check("rtg_render_plan", self.L.lib.rtg_render_plan(self.handle, C.byref(cam), C.byref(job),
+                                                                    C.byref(out)))
+        return out
 
     def render_host(self, cam: rtg_camera_desc, seed: int = DEFAULT_SEED, row_begin: int = 0,
                     row_stride: int = 1, row_count: int = 0, count: bool = False):

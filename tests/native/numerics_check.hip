@@ -27,10 +27,11 @@ __device__ __forceinline__ float rand_float(uint64_t h, int emin, int emax) {
 }
 
 // out[0] division mismatches, out[1] sqrt mismatches (random operands), out[2] sqrt mismatches on
-// the kernel's 1 - z^2 / uniform operands, out[3] operands tested; ex[0..3] the last mismatch seen
+// the kernel's 1 - z^2 / uniform operands, out[3] operands tested, out[4] div_rn_wide mismatches on
+// tiny divisors (2^-149 .. 2^-20, denormals included); ex[0..3] the last mismatch seen
 __global__ void check_kernel(uint64_t n, uint64_t seed, unsigned long long* out, float* ex) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  unsigned long long bad_div = 0, bad_sqrt = 0, bad_kern = 0;
+  unsigned long long bad_div = 0, bad_sqrt = 0, bad_kern = 0, bad_wide = 0;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t h0 = splitmix(seed ^ (i * 4 + 0)), h1 = splitmix(seed ^ (i * 4 + 1));
     const uint64_t h2 = splitmix(seed ^ (i * 4 + 2)), h3 = splitmix(seed ^ (i * 4 + 3));
@@ -44,6 +45,22 @@ __global__ void check_kernel(uint64_t n, uint64_t seed, unsigned long long* out,
     if (__float_as_uint(q) != __float_as_uint(q_ieee)) {
       ++bad_div;
       ex[0] = x, ex[1] = y;
+    }
+    // the sphere test's near root c / q (div_rn_wide): numerators 2^-60 .. 2^40, divisors 2^-126 ..
+    // 2^-20 and denormal ones (1/16 of them), quotients below 2^120 (the kernel's c / q is a
+    // distance compared with tmin and the closest hit)
+    {
+      const float xw = (h2 & 63) == 3 ? 0.0f : rand_float(h3, -60, 40);
+      float yw = rand_float(h0 ^ h1, -126, -20);
+      if (((h1 >> 40) & 15) == 0)  // a denormal divisor
+        yw = __uint_as_float((static_cast<uint32_t>(h0 >> 40) & 0x7fffffu) | 1u | (static_cast<uint32_t>(h1 >> 63) << 31));
+      const float qi = xw / yw;
+      if (fabsf(qi) < 0x1p120f && __float_as_uint(rtg::div_rn_wide(xw, yw)) != __float_as_uint(qi)) {
+        ++bad_wide;
+        ex[0] = xw, ex[1] = yw;
+      }
+      // the common range goes through the unscaled path unchanged
+      if (__float_as_uint(rtg::div_rn_wide(x, y)) != __float_as_uint(q_ieee)) ++bad_wide;
     }
     // square root: 0 and 2^-90 .. 2^100
     float s = fabsf(rand_float(h3, -90, 100));
@@ -66,24 +83,25 @@ __global__ void check_kernel(uint64_t n, uint64_t seed, unsigned long long* out,
   if (bad_div) atomicAdd(&out[0], bad_div);
   if (bad_sqrt) atomicAdd(&out[1], bad_sqrt);
   if (bad_kern) atomicAdd(&out[2], bad_kern);
+  if (bad_wide) atomicAdd(&out[4], bad_wide);
 }
 
 }  // namespace
 
-// n operands of each kind from `seed`; out[4] as in check_kernel, examples[4]. Returns 0 or a HIP error.
-extern "C" int rtg_numerics_check(uint64_t n, uint64_t seed, unsigned long long out[4], float examples[4]) {
+// n operands of each kind from `seed`; out[5] as in check_kernel, examples[4]. Returns 0 or a HIP error.
+extern "C" int rtg_numerics_check(uint64_t n, uint64_t seed, unsigned long long out[5], float examples[4]) {
   unsigned long long* d_out = nullptr;
   float* d_ex = nullptr;
-  hipError_t e = hipMalloc(&d_out, 4 * sizeof(unsigned long long));
+  hipError_t e = hipMalloc(&d_out, 5 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMalloc(&d_ex, 4 * sizeof(float));
-  if (e == hipSuccess) e = hipMemset(d_out, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(d_out, 0, 5 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(d_ex, 0, 4 * sizeof(float));
   if (e == hipSuccess) {
     hipLaunchKernelGGL(check_kernel, dim3(1024), dim3(256), 0, nullptr, n, seed, d_out, d_ex);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(out, d_out, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(out, d_out, 5 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
   if (e == hipSuccess) e = hipMemcpy(examples, d_ex, 4 * sizeof(float), hipMemcpyDeviceToHost);
   out[3] = n;
   if (d_out) (void)hipFree(d_out);

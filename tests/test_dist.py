@@ -1,7 +1,14 @@
-"""Multi-rank path on CPU (gloo, world_size 2 and 3): each rank renders its interleaved shard,
-rtgpu.gather_frame collects and de-interleaves on rank 0, and the frame must equal a single-rank
-render bit for bit — the RNG is keyed by the global pixel id, so tiling cannot change a pixel.
-The per-rank renderer here is the fp32 oracle (the GPU kernel is exercised by test_gpu.py)."""
+"""Multi-rank frame assembly on CPU (gloo, world_size 2 and 3, including ranks past the last row).
+
+Every rank takes its shard from the library's own layout (rtg_shard_layout: rows r, r+N, ...,
+padded to ceil(H/N) rows — the arithmetic rtg_render_frame and rtg_gather_rows use), fills it with a
+code that names the global pixel it holds, and the frame is assembled on rank 0 both ways bench.py
+can do it: (a) the RCCL-gather layout (N padded blocks, one per rank, gathered into one staging
+buffer) de-interleaved by rtg_deinterleave_rows_host, the host twin of the root's de-interleave
+kernel (same index function); (b) rtgpu.gather_frame (torch.distributed.gather, bench.py's default
+N>1 gather). Both must give every pixel its own code, fp32 and RGB8 rows alike. The GPU side of the
+same layout (the de-interleave kernel, the world-of-one RCCL gather, rtg_render_frame over two
+devices where a node has them) is in test_gpu.py."""
 import os
 import socket
 
@@ -18,61 +25,93 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, result_path):
+def _pixel_codes(rows, W):
+    """fp32 code of each pixel (image row, column, channel) of the given image rows."""
+    r = np.asarray(rows, dtype=np.float32)[:, None, None]
+    c = np.arange(W, dtype=np.float32)[None, :, None]
+    ch = np.arange(3, dtype=np.float32)[None, None, :]
+    return r * 4096.0 + c * 4.0 + ch
+
+
+def _worker(rank, world, port, H, W, result_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import rtgpu
-        from oracle_bind import Oracle
 
-        s = rtgpu.SceneLibrary().build("bouncing_spheres", rand_seed=1)
-        cam = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
-        cam.image_width, cam.samples_per_pixel, cam.max_depth = 40, 2, 10
-        H = rtgpu.Library().camera_resolve(cam).image_height
-        b, stride, n = rtgpu.shard_rows(H, rank, world)
-        rows = rtgpu.padded_rows(H, world)
-        shard = torch.zeros((rows, 40, 3), dtype=torch.float32)
+        lib = rtgpu.Library()
+        b, stride, n, padded = lib.shard_layout(H, world, rank)
+        assert (b, stride, n) == rtgpu.shard_rows(H, rank, world) and padded == rtgpu.padded_rows(H, world)
+        shard = torch.full((padded, W, 3), -1.0, dtype=torch.float32)  # padding rows stay -1
         if n:
-            img, _ = Oracle().render_f32(s.desc, cam, row_begin=b, row_stride=stride, row_count=n)
-            shard[:n] = torch.from_numpy(img)
-        frame = rtgpu.gather_frame(shard, H)
-        # the RGB8 variant: write_color bytes gathered, 4x fewer bytes
-        bytes8 = torch.from_numpy(np.stack([rtgpu.write_color_bytes(r) for r in shard.numpy()]))
-        frame8 = rtgpu.gather_frame(bytes8, H)
+            shard[:n] = torch.from_numpy(_pixel_codes([b + k * stride for k in range(n)], W))
+        # (a) the RCCL layout: N padded blocks gathered into one staging buffer, host de-interleave
+        blocks = [torch.empty_like(shard) for _ in range(world)] if rank == 0 else None
+        dist.gather(shard, gather_list=blocks, dst=0)
+        # (b) bench.py's default torch.distributed gather + torch de-interleave
+        frame_t = rtgpu.gather_frame(shard, H)
+        # RGB8 rows (write_color bytes, 3 B per pixel: rows of W*3 bytes, not a multiple of 16)
+        bytes8 = torch.from_numpy(rtgpu.write_color_bytes(shard.numpy() / 8192.0))
+        blocks8 = [torch.empty_like(bytes8) for _ in range(world)] if rank == 0 else None
+        dist.gather(bytes8, gather_list=blocks8, dst=0)
         if rank == 0:
-            np.save(result_path, frame.numpy())
-            np.save(result_path + ".rgb8.npy", frame8.numpy())
+            stage = torch.cat(blocks).numpy()
+            np.save(result_path, lib.deinterleave_rows_host(stage, world, H))
+            np.save(result_path + ".torch.npy", frame_t.numpy())
+            np.save(result_path + ".rgb8.npy", lib.deinterleave_rows_host(torch.cat(blocks8).numpy(), world, H))
         else:
-            assert frame is None and frame8 is None
+            assert frame_t is None
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_sharded_render_equals_single(tmp_path, world, scenes, oracle, lib):
-    import rtgpu
-
+@pytest.mark.parametrize("world,H", [(2, 225), (3, 224), (3, 2)])
+def test_gloo_frame_assembly_uses_the_library_layout(tmp_path, world, H):
+    W = 40
     out = str(tmp_path / "frame.npy")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), H, W, out), nprocs=world, join=True)
+    want = _pixel_codes(range(H), W)
     frame = np.load(out)
-    s = scenes.build("bouncing_spheres", rand_seed=1)
-    cam = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
-    cam.image_width, cam.samples_per_pixel, cam.max_depth = 40, 2, 10
-    full, _ = oracle.render_f32(s.desc, cam)
-    assert frame.shape == full.shape
-    assert np.array_equal(frame, full)
-    frame8 = np.load(out + ".rgb8.npy")
-    assert frame8.dtype == np.uint8 and np.array_equal(frame8, rtgpu.write_color_bytes(full))
-
-
-def test_shard_rows_cover_the_image():
+    assert frame.shape == (H, W, 3) and np.array_equal(frame, want)
+    assert np.array_equal(np.load(out + ".torch.npy"), want)
     import rtgpu
 
-    for H in (1, 7, 225, 1080, 2160):
+    assert np.array_equal(np.load(out + ".rgb8.npy"), rtgpu.write_color_bytes(want / 8192.0))
+
+
+def test_shard_layout_matches_python_and_covers_the_image(lib):
+    """rtg_shard_layout (C) = rtgpu.shard_rows / padded_rows (Python, bench.py), and the shards of
+    every rank cover each image row exactly once, for image heights below, at and above N."""
+    import rtgpu
+
+    for H in (1, 2, 7, 225, 1080, 2160):
         for world in (1, 2, 3, 4, 8, 16):
             rows = []
             for r in range(world):
-                b, stride, n = rtgpu.shard_rows(H, r, world)
+                b, stride, n, padded = lib.shard_layout(H, world, r)
+                assert (b, stride, n) == rtgpu.shard_rows(H, r, world)
+                assert padded == rtgpu.padded_rows(H, world) and n <= padded
                 rows += [b + k * stride for k in range(n)]
-                assert n <= rtgpu.padded_rows(H, world)
             assert sorted(rows) == list(range(H))
+
+
+def test_host_deinterleave_matches_numpy(lib):
+    """The host twin of the de-interleave kernel against rtgpu.deinterleave (numpy) on byte rows of
+    every width class (16-B multiples and not) and ranks past the last row."""
+    import rtgpu
+
+    rng = np.random.default_rng(3)
+    for H, world, W in ((1080, 8, 16), (7, 3, 5), (2, 5, 3), (13, 4, 1)):
+        padded = rtgpu.padded_rows(H, world)
+        blocks = rng.integers(0, 255, size=(world, padded, W, 3), dtype=np.uint8)
+        want = rtgpu.deinterleave(list(blocks), H)
+        got = lib.deinterleave_rows_host(blocks.reshape(world * padded, W, 3), world, H)
+        assert np.array_equal(got, want)
+
+
+def test_bad_layout_arguments_are_rejected(lib):
+    import rtgpu
+
+    for args in ((0, 2, 0), (10, 0, 0), (10, 2, 2), (10, 2, -1)):
+        with pytest.raises(rtgpu.RtgError):
+            lib.shard_layout(*args)

@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--write-binding", default=None,
                     help="write the binding-resource summary bench.py attaches (profiles/pmc_binding.json)")
     ap.add_argument("--simds", type=int, default=1024, help="SIMDs of the chip (256 CUs x 4)")
+    ap.add_argument("--counted-launch", default="the render kernel's single launch",
+                    help="which launch the counters saw (config 2: the 16-wave launch alone, RTG_DUAL=0)")
     a = ap.parse_args()
     counters, info = {}, {}
     for sub in sorted(os.listdir(a.prof_dir)):
@@ -104,33 +106,47 @@ def main():
         out["valu_issue_frac"] = 2 * avg["SQ_INSTS_VALU"] / (a.simds * cycles)
         if "valu_lane_utilization" in out:
             out["useful_valu_frac"] = out["valu_issue_frac"] * out["valu_lane_utilization"]
+    if "TA_BUSY_avr" in avg and "GRBM_GUI_ACTIVE" in avg:
+        out["ta_busy_frac"] = avg["TA_BUSY_avr"] / (avg["GRBM_GUI_ACTIVE"] / 8)
     if "SQ_LDS_BANK_CONFLICT" in avg and "SQ_ACTIVE_INST_LDS" in avg:
         out["lds_bank_conflict_per_lds_cycle"] = avg["SQ_LDS_BANK_CONFLICT"] / max(1.0, avg["SQ_ACTIVE_INST_LDS"])
     print(json.dumps(out, indent=1))
     if a.write_traffic and "hbm_bytes_per_launch" in out:
-        with open(a.write_traffic, "w") as f:
-            json.dump({"workload": a.workload, "hbm_bytes_per_launch": int(out["hbm_bytes_per_launch"]),
-                       "hbm_read_bytes": int(out["hbm_read_bytes"]),
-                       "hbm_write_bytes": int(out["hbm_write_bytes"]),
-                       "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                                 "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM"}, f, indent=1)
+        merge_record(a.write_traffic, {
+            "workload": a.workload, "hbm_bytes_per_launch": int(out["hbm_bytes_per_launch"]),
+            "hbm_read_bytes": int(out["hbm_read_bytes"]), "hbm_write_bytes": int(out["hbm_write_bytes"]),
+            "counted_launch": a.counted_launch, "profile_dir": a.prof_dir,
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                      "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM"})
     if a.write_binding:
         keys = ("valu_issue_frac", "valu_lane_utilization", "useful_valu_frac", "wave_cycle_split",
-                "lds_bank_conflict_per_lds_cycle", "l2_hit_rate", "effective_clock_ghz")
+                "lds_bank_conflict_per_lds_cycle", "l2_hit_rate", "effective_clock_ghz", "ta_busy_frac")
         rec = {"workload": a.workload, "kernel_ns": round(ns_avg),
                **{k: out[k] for k in keys if k in out},
-               "vgpr": next(iter(out["dispatch"].values()))["vgpr"] if out["dispatch"] else None,
-               "launch": "the 16-wave persistent launch alone (RTG_DUAL=0): counter collection serialises the "
-                         "dual launch's two dispatches (DESIGN.md §6)",
+               "sq_insts_valu_per_launch": avg.get("SQ_INSTS_VALU"),
+               "counted_launch": a.counted_launch, "profile_dir": a.prof_dir,
                "source": "rocprofv3 --pmc passes of tools/profile.sh (SQ_INSTS_VALU, SQ_THREAD_CYCLES_VALU, "
                          "SQ_ACTIVE_INST_VALU, SQ_WAVE_CYCLES, SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY, "
-                         "SQ_LDS_BANK_CONFLICT, SQ_ACTIVE_INST_LDS, GRBM_GUI_ACTIVE, TCC_HIT/MISS)",
-               "reading": "valu_issue_frac = 2 cycles x SQ_INSTS_VALU / (1024 SIMDs x kernel cycles); "
-                          "useful_valu_frac = that x lane utilisation: the fraction of the chip's fp32 "
-                          "lane-issue slots doing path-tracing work (DESIGN.md §6)"}
-        with open(a.write_binding, "w") as f:
-            json.dump(rec, f, indent=1)
+                         "SQ_LDS_BANK_CONFLICT, SQ_ACTIVE_INST_LDS, GRBM_GUI_ACTIVE, TCC_HIT/MISS, TA_BUSY)",
+               "reading": "valu_issue_frac = 2 cycles x SQ_INSTS_VALU / (1024 SIMDs x kernel cycles of the counted "
+                          "launch); useful_valu_frac = that x lane utilisation: the fraction of the chip's fp32 "
+                          "lane-issue slots doing path-tracing work (DESIGN.md §6). bench.py re-derives both for "
+                          "the timed launch (valu_issue_frac_timed) from the counted instructions"}
+        merge_record(a.write_binding, rec)
     return 0
+
+
+def merge_record(path, rec):
+    """Add or replace rec (keyed by workload) in a {"records": [...]} file."""
+    try:
+        with open(path) as f:
+            doc = json.load(f)
+    except (OSError, ValueError):
+        doc = {}
+    recs = [r for r in doc.get("records", [doc] if doc.get("workload") else []) if r.get("workload") != rec["workload"]]
+    recs.append(rec)
+    with open(path, "w") as f:
+        json.dump({"records": recs}, f, indent=1)
 
 
 if __name__ == "__main__":

@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p "$OUT"
 BENCH=(python3 bench.py --steps "${STEPS:-3}" --warmup 1 --no-cpu-baseline "$@")
 PMC_BENCH=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@")
@@ -36,4 +36,6 @@ run pmc_sq2 600 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_A
     -f csv -d "$OUT/pmc_sq2" -o run -- "${PMC_BENCH[@]}" || exit $?
 run pmc_cache 600 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum \
     -f csv -d "$OUT/pmc_cache" -o run -- "${PMC_BENCH[@]}" || exit $?
+run pmc_ta 600 --pmc TA_BUSY_avr GRBM_GUI_ACTIVE \
+    -f csv -d "$OUT/pmc_ta" -o run -- "${PMC_BENCH[@]}" || exit $?
 exit 0

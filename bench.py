@@ -68,6 +68,9 @@ def parse():
                     help="N>1 timed gather: torch.distributed.gather + a torch de-interleave (default until the "
                          "C-ABI path has run on a multi-GPU node) or the C-ABI's RCCL gather + de-interleave "
                          "kernel (rtg_gather_rows)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N>1 process group: nccl (= RCCL, one rank per GPU) or gloo (rehearsal of the N>1 flow "
+                         "with several ranks on one GPU; the frame is gathered through host memory)")
     ap.add_argument("--no-rtg-check", action="store_true",
                     help="N>1: skip the untimed rtg_gather_rows cross-check of the last frame")
     ap.add_argument("--check-timeout", type=float, default=180.0,
@@ -115,7 +118,7 @@ def host_cpus():
 
 # scenes the ref-hybrid harness builds from the reference's own geometry code
 HARNESS_SCENE = {("bouncing_spheres", 11): "book1", ("cornell_box", 0): "cornell",
-                 ("bouncing_spheres", 500): "book1_g500"}
+                 ("bouncing_spheres", 500): "book1_g500", ("earth_perlin", 0): "earth_perlin"}
 
 
 def _cpu_run(args, scene_desc, cam, procs, spp, row_step):
@@ -295,10 +298,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    gloo = args.dist_backend == "gloo"
+    if gloo:
+        if args.gather_impl == "rtg":
+            sys.exit("--dist-backend gloo gathers through host memory: use --gather-impl torch")
+        local = local % max(1, torch.cuda.device_count())  # several ranks may share one GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        if gloo:  # rehearsal of the N > 1 flow with several ranks on one GPU (tests/test_gpu.py)
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", local))
 
     lib = rtgpu.Library()
     scenes = rtgpu.SceneLibrary()
@@ -347,7 +358,7 @@ def main():
                                  frame.data_ptr() if frame is not None else 0, [stream])
                 gathered[0] = frame
             else:
-                gathered[0] = rtgpu.gather_frame(src, H)
+                gathered[0] = rtgpu.gather_frame(src.cpu() if gloo else src, H)
             g1.record()
         return st
 
@@ -379,8 +390,8 @@ def main():
         elif rank == 0 and gathered[0] is not None:
             last_frame = gathered[0].cpu().numpy()
 
-    tot = torch.tensor([float(segs)], dtype=torch.float64, device="cuda")
-    tmax = torch.tensor([dt], dtype=torch.float64, device="cuda")
+    tot = torch.tensor([float(segs)], dtype=torch.float64, device="cpu" if gloo else "cuda")
+    tmax = torch.tensor([dt], dtype=torch.float64, device="cpu" if gloo else "cuda")
     if world > 1:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -498,7 +509,7 @@ def main():
             if world > 1:
                 line["parity"]["frame"] = f"gathered on rank 0 from {world} ranks"
 
-    if world > 1 and not args.no_rtg_check:
+    if world > 1 and not args.no_rtg_check and not gloo:
         # the C-ABI's RCCL gather, untimed, on the last frame's shards: byte-compared with the timed frame
         def give_up():
             if rank == 0:

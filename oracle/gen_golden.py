@@ -41,6 +41,8 @@ HYBRID_RENDERS = [
     ("cornell_translate", 40, 40, 8, 100, 9),  # the reference's translate class (hittable.hpp:74-117)
     ("simple_light", 64, 36, 8, 20, 5),
     ("perlin", 64, 36, 4, 10, 7),
+    ("earth", 64, 36, 4, 10, 11),  # image_texture on the committed texels (texture.hpp:91-122)
+    ("earth_perlin", 64, 36, 4, 20, 13),  # BASELINE config 3's scene
 ]
 
 # G5: (scene, W, H, spp per process, processes, depth). book1 = BASELINE config-1
@@ -54,6 +56,8 @@ MOMENTS = [
     ("simple_light", 192, 108, 512, 8, 50),
     ("perlin", 160, 90, 256, 8, 50),
     ("book1_g500", 96, 54, 256, 8, 50),
+    ("earth_perlin", 192, 108, 512, 8, 50),  # BASELINE config 3's scene: image + noise textures
+    ("earth", 128, 72, 512, 8, 50),
 ]
 MOMENTS_SEED0 = 90001
 

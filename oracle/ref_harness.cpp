@@ -82,6 +82,82 @@ class noise_texture : public texture {
   double scale;
 };
 
+// rtw_image (rtw_stb_image.hpp:28-178) restated on the committed decoded texels: stb_image is absent
+// (hazard H11), so tests/golden/earthmap.ppm holds earthmap.jpg decoded to 8-bit sRGB, and the load
+// applies stbi_loadf's ldr-to-hdr step (pow(b / 255, 2.2), C double pow as in stb) then
+// float_to_byte (rtw_stb_image.hpp:137-150), exactly the bytes rtw_image::convert_to_bytes keeps.
+// pixel_data keeps the reference's clamp (x = high - 1 past the edge) and magenta fallback.
+class rtw_image_ppm {
+ public:
+  explicit rtw_image_ppm(const std::string& path) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) {
+      std::fprintf(stderr, "ref_harness: cannot open %s\n", path.c_str());
+      return;
+    }
+    int w = 0, h = 0, maxv = 0;
+    char magic[3] = {0, 0, 0};
+    if (std::fscanf(f, "%2s %d %d %d", magic, &w, &h, &maxv) == 4 && std::string(magic) == "P6" && maxv == 255 &&
+        std::fgetc(f) != EOF) {
+      std::vector<unsigned char> b(static_cast<size_t>(w) * h * 3);
+      if (std::fread(b.data(), 1, b.size(), f) == b.size()) {
+        for (auto& x : b) x = float_to_byte(static_cast<float>(::pow(x / 255.0f, 2.2f) * 1.0f));
+        bdata.swap(b);
+        image_width = w;
+        image_height = h;
+      }
+    }
+    std::fclose(f);
+  }
+  int width() const { return bdata.empty() ? 0 : image_width; }
+  int height() const { return bdata.empty() ? 0 : image_height; }
+  const unsigned char* pixel_data(int x, int y) const {
+    static unsigned char magenta[] = {255, 0, 255};
+    if (bdata.empty()) return magenta;
+    x = clamp(x, 0, image_width);
+    y = clamp(y, 0, image_height);
+    return bdata.data() + y * image_width * 3 + x * 3;
+  }
+
+ private:
+  static int clamp(int x, int low, int high) { return x < low ? low : (x < high ? x : high - 1); }
+  static unsigned char float_to_byte(float value) {
+    if (value <= 0.0f) return 0;
+    if (value >= 1.0f) return 255;
+    return static_cast<unsigned char>(256.0f * value);
+  }
+  std::vector<unsigned char> bdata;
+  int image_width = 0, image_height = 0;
+};
+
+// tests/golden/earthmap.ppm: $RTG_EARTHMAP, else relative to this executable (oracle/_ref/)
+static std::string earthmap_path() {
+  if (const char* e = std::getenv("RTG_EARTHMAP")) return e;
+  char buf[4096];
+  const ssize_t n = readlink("/proc/self/exe", buf, sizeof(buf) - 1);
+  std::string exe = n > 0 ? std::string(buf, static_cast<size_t>(n)) : std::string("oracle/_ref/ref_harness");
+  return exe.substr(0, exe.find_last_of('/')) + "/../../tests/golden/earthmap.ppm";
+}
+
+// image_texture::value (texture.hpp:97-118)
+class image_texture : public texture {
+ public:
+  explicit image_texture(const std::string& path) : image(path) {}
+  color value(double u, double v, const point3&) const override {
+    if (image.height() <= 0) return color(0.0f, 1.0f, 1.0f);
+    u = interval(0.0f, 1.0f).clamp(u);
+    v = 1.0f - interval(0.0f, 1.0f).clamp(v);
+    auto i = int(u * image.width());
+    auto j = int(v * image.height());
+    auto pixel = image.pixel_data(i, j);
+    auto color_scale = 1.0f / 255.0f;
+    return color(color_scale * pixel[0], color_scale * pixel[1], color_scale * pixel[2]);
+  }
+
+ private:
+  rtw_image_ppm image;
+};
+
 class material {
  public:
   virtual ~material() = default;
@@ -347,7 +423,9 @@ static void setup_cam(const std::string& scene, cam_t& c) {
     c.background = color(0.0f, 0.0f, 0.0f);
     c.lookfrom = point3(26.0f, 3.0f, 6.0f);
     c.lookat = point3(0.0f, 2.0f, 0.0f);
-  }
+  } else if (scene == "earth") {  // main.cpp:157-166
+    c.lookfrom = point3(0.0f, 0.0f, 12.0f);
+  }  // earth_perlin (BASELINE config 3): perlin_sphere's camera, main.cpp:190-201
 }
 
 static std::shared_ptr<hittable> make_world(const std::string& scene) {
@@ -381,6 +459,14 @@ static std::shared_ptr<hittable> make_world(const std::string& scene) {
       w->add(std::make_shared<translate>(std::make_shared<sphere>(point3(0.0f, 0.0f, 0.0f), 60.0f, chrome),
                                          vec3(420.0f, 90.0f, 120.0f)));
     }
+  } else if (scene == "earth") {  // main.cpp:141-171
+    auto surface = std::make_shared<lambertian>(std::make_shared<image_texture>(earthmap_path()));
+    w->add(std::make_shared<sphere>(point3(0.0f, 0.0f, 0.0f), 2.0f, surface));
+  } else if (scene == "earth_perlin") {  // BASELINE config 3: perlin ground, then the globe
+    auto pertext = std::make_shared<noise_texture>(4);  // perlin tables first from the seed-1 stream
+    w->add(std::make_shared<sphere>(point3(0.0f, -1000.0f, 0.0f), 1000.0f, std::make_shared<lambertian>(pertext)));
+    auto globe = std::make_shared<lambertian>(std::make_shared<image_texture>(earthmap_path()));
+    w->add(std::make_shared<sphere>(point3(0.0f, 2.0f, 0.0f), 2.0f, globe));
   } else if (scene == "simple_light" || scene == "perlin") {  // main.cpp:174-207, 254-298
     auto pertext = std::make_shared<noise_texture>(4);
     w->add(std::make_shared<sphere>(point3(0.0f, -1000.0f, 0.0f), 1000.0f, std::make_shared<lambertian>(pertext)));

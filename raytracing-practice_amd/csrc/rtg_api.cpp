@@ -246,6 +246,16 @@ void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
 }
 
 bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
+  // phase timings of the host compile (RTG_VERBOSE): config 5's 1M spheres make these the setup cost
+  const bool verbose = std::getenv("RTG_VERBOSE") != nullptr;
+  auto tp = std::chrono::steady_clock::now();
+  auto phase = [&](const char* what) {
+    const auto now = std::chrono::steady_clock::now();
+    if (verbose)
+      std::fprintf(stderr, "[rtg] compile %-10s %8.1f ms\n", what,
+                   std::chrono::duration<double, std::milli>(now - tp).count());
+    tp = now;
+  };
   if (d->num_prims < 0 || (d->num_prims > 0 && !d->prims) || d->num_materials < 0 ||
       (d->num_materials > 0 && !d->materials) || d->num_textures < 0 ||
       (d->num_textures > 0 && !d->textures) || d->num_images < 0 ||
@@ -323,7 +333,9 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       bd.prims = rest.data();
       bd.num_prims = d->num_prims - 1;
     }
+    phase("validate");
     if (!build_bvh(&bd, &bvh, err)) return false;
+    phase("bvh");
     if (occ >= 0)  // refs back to input indices
       for (auto& r : bvh.refs) r = r >= occ ? r + 1 : r;
   }
@@ -342,7 +354,9 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->stack_need = 0;
   } else if (d->bvh_mode == RTG_BVH_SAH && !bvh.nodes.empty()) {
     collapse_bvh4(bvh, &bvh4);
+    phase("collapse");
     reorder_top_bfs(&bvh4, kTreeletBfsNodes);
+    phase("bfs");
     out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
     out->depth = bvh4.depth;
     out->stack_need = bvh4.max_pushes;
@@ -405,6 +419,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->spheres.insert(out->spheres.end(), rec, rec + 8);
   }
 
+  phase("prims");
   // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
   auto leaf_code = [&](int32_t child, int32_t count, int32_t* code) {
     const int64_t first = -(static_cast<int64_t>(child) + 1);
@@ -500,6 +515,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     f[15] = 0.0f;
   }
 
+  phase("nodes");
   // materials {type, texture, fuzz, eta}, {albedo.xyz, uses_uv}. A lambertian or diffuse_light whose
   // texture is a solid_color carries the colour itself (texture -1, albedo = the colour: the value
   // solid_color::value returns, texture.hpp:34-44), and only the textures some material still
@@ -596,6 +612,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_y, pl.perm_y + 256);
     out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_z, pl.perm_z + 256);
   }
+  phase("materials");
   return true;
 }
 

@@ -16,6 +16,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
+#include <new>
+#include <thread>
 
 #include "rtg_internal.hpp"
 
@@ -77,6 +79,22 @@ double half_area(const Box& b) {
   const double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
   if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
   return dx * dy + dy * dz + dz * dx;
+}
+
+// Data-parallel loop over [start, end) in T contiguous chunks (T-1 helper threads + this one).
+template <class F>
+void par_chunks(int64_t start, int64_t end, int T, F&& f) {
+  if (T <= 1) {
+    f(start, end, 0);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  const int64_t n = end - start;
+  for (int t = 1; t < T; ++t)
+    th.emplace_back([&, t]() { f(start + n * t / T, start + n * (t + 1) / T, t); });
+  f(start, start + n / T, 0);
+  for (auto& x : th) x.join();
 }
 
 struct Builder {
@@ -148,73 +166,237 @@ struct Builder {
     return node;
   }
 
-  // ---- binned SAH ----
-  static constexpr int kMaxBins = 64;
-  // 32 bins on all three axes (round 2; round 1: 16 on the longest centroid axis): book-1 -2.3 %,
-  // Cornell -5 %, config 5 -0.5 %, +1.5 s of host build for 1M spheres
-  int kBins = 32;          // centroid bins per axis
+};
+
+// ---- binned SAH (RTG_BVH_SAH) ----
+// Primitives travel with their boxes (one contiguous 56-B record each) instead of through an index
+// array, and one pass per node bins every primitive on all three axes, keeping per bin the box, the
+// centroid box and the count: the split's child boxes and child centroid boxes are unions of bins,
+// so a node costs the binning pass and the partition (it was seven passes). Subtrees of large ranges
+// build concurrently into their own buffers and are spliced back in depth-first order; the loops of
+// the top levels run on the builder's threads. Unions are exact min / max and counts integers, and
+// the partition is the sequential std::partition, so the tree is node for node the one the
+// single-thread builder of round 2 produced (tests/test_host.py pins the hash).
+struct PrimRec {
+  double lo[3], hi[3];
+  int64_t id;
+};
+
+struct SahBuilder {
+  std::vector<PrimRec>& p;
+  Bvh& out;
+  int threads = 1;
+  int kBins = 32;          // centroid bins per axis (round 2: 32 on all three axes; round 1: 16 on one)
   int axes = 3;            // 1: the centroid box's longest axis only, 3: the best split over all three
   int kMaxLeaf = 4;        // primitives per leaf (<= 8, the leaf code's count field)
   double trav_cost = 0.5;  // cost of one more level relative to one primitive test (measured best)
+  bool parallel = false;   // build subtrees of large ranges concurrently
+  static constexpr int kMaxBins = 64;
+  static constexpr int64_t kParMin = 65536;    // ranges whose loops run data-parallel
+  static constexpr int64_t kSpawnMin = 32768;  // ranges whose two subtrees build concurrently
 
-  // Returns a child code for the range; `node_depth` = depth of the node that would own it.
-  int32_t sah_child(int64_t start, int64_t end, const Box& bbox, int depth, int32_t* count) {
+  struct Bin {
+    Box box, cbox;
+    int64_t n = 0;
+  };
+  struct AxisBins {
+    Bin b[3][kMaxBins];
+  };
+
+  static void add_point(Box& b, const double c[3]) {
+    for (int k = 0; k < 3; ++k) {
+      b.lo[k] = std::min(b.lo[k], c[k]);
+      b.hi[k] = std::max(b.hi[k], c[k]);
+    }
+  }
+  static void centroid(const PrimRec& r, double c[3]) {
+    for (int k = 0; k < 3; ++k) c[k] = 0.5 * (r.lo[k] + r.hi[k]);
+  }
+  static Box box_of(const PrimRec& r) {
+    Box b;
+    for (int k = 0; k < 3; ++k) {
+      b.lo[k] = r.lo[k];
+      b.hi[k] = r.hi[k];
+    }
+    return b;
+  }
+
+  int32_t leaf(int64_t first, int64_t count) {
+    const int64_t slot = static_cast<int64_t>(out.refs.size());
+    for (int64_t i = 0; i < count; ++i) out.refs.push_back(p[first + i].id);
+    return -(1 + static_cast<int32_t>(slot));
+  }
+  int32_t new_node() {
+    BuildNode n;
+    for (int s = 0; s < 2; ++s) {
+      n.child[s] = kEmptyChild;
+      n.count[s] = 0;
+      for (int k = 0; k < 3; ++k) {
+        n.lo[s][k] = kInf;
+        n.hi[s][k] = -kInf;
+      }
+    }
+    out.nodes.push_back(n);
+    return static_cast<int32_t>(out.nodes.size() - 1);
+  }
+  void set_child(int32_t node, int side, int32_t code, int32_t count, const Box& b) {
+    BuildNode& n = out.nodes[node];
+    n.child[side] = code;
+    n.count[side] = count;
+    for (int k = 0; k < 3; ++k) {
+      n.lo[side][k] = b.lo[k];
+      n.hi[side][k] = b.hi[k];
+    }
+  }
+
+  // box and centroid box of a range (root, and the rare degenerate split)
+  void range_boxes(int64_t start, int64_t end, Box* bb, Box* cb) const {
+    const int T = end - start >= kParMin ? threads : 1;
+    std::vector<Box> pb(T), pc(T);
+    par_chunks(start, end, T, [&](int64_t a, int64_t e, int t) {
+      Box b, c;
+      for (int64_t i = a; i < e; ++i) {
+        double m[3];
+        centroid(p[i], m);
+        b = box_union(b, box_of(p[i]));
+        add_point(c, m);
+      }
+      pb[t] = b;
+      pc[t] = c;
+    });
+    *bb = Box{};
+    *cb = Box{};
+    for (int t = 0; t < T; ++t) {
+      *bb = box_union(*bb, pb[t]);
+      *cb = box_union(*cb, pc[t]);
+    }
+  }
+
+  // Returns a child code for the range [start, end) with box `bbox` and centroid box `cb`.
+  int32_t sah_child(int64_t start, int64_t end, const Box& bbox, const Box& cb, int depth, int32_t* count) {
     const int64_t n = end - start;
     if (n <= 1) {
       *count = static_cast<int32_t>(n);
       return leaf(start, n);
     }
     int64_t mid = -1;
-    Box cb;
-    for (int64_t i = start; i < end; ++i) {
-      const Box& b = boxes[ids[i]];
-      for (int k = 0; k < 3; ++k) {
-        const double c = 0.5 * (b.lo[k] + b.hi[k]);
-        cb.lo[k] = std::min(cb.lo[k], c);
-        cb.hi[k] = std::max(cb.hi[k], c);
-      }
-    }
     const int long_axis = longest_axis(cb);
     int axis = long_axis;
     const double leaf_cost = static_cast<double>(n) * half_area(bbox);
+    Box lb, rb, lcb, rcb;
+    bool child_boxes = false;
     if (cb.hi[long_axis] - cb.lo[long_axis] > 0.0) {
-      // binned SAH over the longest centroid axis (or all three): the best bin boundary
-      double best = kInf;
-      int best_split = -1, best_axis = long_axis;
+      bool use[3] = {false, false, false};
+      double k1[3] = {0.0, 0.0, 0.0};
       for (int ai = 0; ai < (axes == 3 ? 3 : 1); ++ai) {
         const int ax = axes == 3 ? ai : long_axis;
         const double extent = cb.hi[ax] - cb.lo[ax];
         if (!(extent > 0.0)) continue;
-        Box bin_box[kMaxBins];
-        int64_t bin_n[kMaxBins] = {0};
-        const double k1 = kBins * (1.0 - 1e-9) / extent;
-        for (int64_t i = start; i < end; ++i) {
-          const Box& b = boxes[ids[i]];
-          int bi = static_cast<int>((0.5 * (b.lo[ax] + b.hi[ax]) - cb.lo[ax]) * k1);
-          bi = std::min(std::max(bi, 0), kBins - 1);
-          bin_n[bi]++;
-          bin_box[bi] = box_union(bin_box[bi], b);
+        use[ax] = true;
+        k1[ax] = kBins * (1.0 - 1e-9) / extent;
+      }
+      auto bin_of = [&](double c, int ax) {
+        const int bi = static_cast<int>((c - cb.lo[ax]) * k1[ax]);
+        return std::min(std::max(bi, 0), kBins - 1);
+      };
+      // bins are initialised on first touch and the sweeps visit the occupied ones only: a split
+      // between two occupied bins costs the same wherever it falls between them, and the cost loop
+      // keeps the first (strict <), i.e. the bin right after the lower one: the same split as a sweep
+      // over every bin, without its fixed cost on the ~800k small nodes of a 1M-primitive tree
+      Bin* bins[3];
+      uint64_t occ[3] = {0, 0, 0};
+      // uninitialised storage (a Bin's boxes start empty only when first touched: constructing all
+      // 3 x 64 bins per node would write 20 KB for every node of the tree)
+      alignas(Bin) unsigned char local_raw[sizeof(Bin) * 3 * kMaxBins];
+      Bin* local = reinterpret_cast<Bin*>(local_raw);
+      std::vector<AxisBins> part;
+      const int T = n >= kParMin ? threads : 1;
+      auto touch = [](Bin& bn, uint64_t& mask, int bi) {
+        if (!(mask >> bi & 1)) {
+          mask |= uint64_t(1) << bi;
+          new (&bn) Bin();
         }
+      };
+      if (T == 1) {
+        for (int ax = 0; ax < 3; ++ax) bins[ax] = local + ax * kMaxBins;
+        for (int64_t i = start; i < end; ++i) {
+          const PrimRec& r = p[i];
+          double m[3];
+          centroid(r, m);
+          const Box bx = box_of(r);
+          for (int ax = 0; ax < 3; ++ax) {
+            if (!use[ax]) continue;
+            const int bi = bin_of(m[ax], ax);
+            Bin& bn = bins[ax][bi];
+            touch(bn, occ[ax], bi);
+            bn.n++;
+            bn.box = box_union(bn.box, bx);
+            add_point(bn.cbox, m);
+          }
+        }
+      } else {
+        part.resize(T);
+        std::vector<std::array<uint64_t, 3>> pocc(T, std::array<uint64_t, 3>{0, 0, 0});
+        par_chunks(start, end, T, [&](int64_t a, int64_t e, int t) {
+          AxisBins& ab = part[t];
+          for (int64_t i = a; i < e; ++i) {
+            const PrimRec& r = p[i];
+            double m[3];
+            centroid(r, m);
+            const Box bx = box_of(r);
+            for (int ax = 0; ax < 3; ++ax) {
+              if (!use[ax]) continue;
+              const int bi = bin_of(m[ax], ax);
+              Bin& bn = ab.b[ax][bi];
+              touch(bn, pocc[t][ax], bi);
+              bn.n++;
+              bn.box = box_union(bn.box, bx);
+              add_point(bn.cbox, m);
+            }
+          }
+        });
+        for (int ax = 0; ax < 3; ++ax) {
+          bins[ax] = part[0].b[ax];
+          occ[ax] = pocc[0][ax];
+          for (int t = 1; t < T; ++t)
+            for (int k = 0; k < kBins; ++k) {
+              if (!(pocc[t][ax] >> k & 1)) continue;
+              Bin& d = bins[ax][k];
+              touch(d, occ[ax], k);
+              const Bin& s = part[t].b[ax][k];
+              d.n += s.n;
+              d.box = box_union(d.box, s.box);
+              d.cbox = box_union(d.cbox, s.cbox);
+            }
+        }
+      }
+      // the best bin boundary: the round-2 cost loop (axes in order, strict <: ties keep the first)
+      double best = kInf;
+      int best_split = -1, best_axis = long_axis;
+      for (int ai = 0; ai < (axes == 3 ? 3 : 1); ++ai) {
+        const int ax = axes == 3 ? ai : long_axis;
+        if (!use[ax]) continue;
+        int o[kMaxBins], m = 0;
+        for (uint64_t w = occ[ax]; w; w &= w - 1) o[m++] = __builtin_ctzll(w);
         double right_area[kMaxBins];
         int64_t right_n[kMaxBins];
         Box acc;
         int64_t accn = 0;
-        for (int b = kBins - 1; b > 0; --b) {
-          acc = box_union(acc, bin_box[b]);
-          accn += bin_n[b];
-          right_area[b] = half_area(acc);
-          right_n[b] = accn;
+        for (int j = m - 1; j > 0; --j) {
+          acc = box_union(acc, bins[ax][o[j]].box);
+          accn += bins[ax][o[j]].n;
+          right_area[j] = half_area(acc);
+          right_n[j] = accn;
         }
         Box lacc;
         int64_t lacc_n = 0;
-        for (int b = 1; b < kBins; ++b) {
-          lacc = box_union(lacc, bin_box[b - 1]);
-          lacc_n += bin_n[b - 1];
-          if (lacc_n == 0 || right_n[b] == 0) continue;
-          const double cost = half_area(lacc) * lacc_n + right_area[b] * right_n[b];
+        for (int j = 1; j < m; ++j) {
+          lacc = box_union(lacc, bins[ax][o[j - 1]].box);
+          lacc_n += bins[ax][o[j - 1]].n;
+          const double cost = half_area(lacc) * lacc_n + right_area[j] * right_n[j];
           if (cost < best) {
             best = cost;
-            best_split = b;
+            best_split = o[j - 1] + 1;
             best_axis = ax;
           }
         }
@@ -226,37 +408,80 @@ struct Builder {
       }
       if (best_split > 0) {
         axis = best_axis;
-        const double k1 = kBins * (1.0 - 1e-9) / (cb.hi[axis] - cb.lo[axis]);
-        auto it = std::partition(ids.begin() + start, ids.begin() + end, [&](int64_t id) {
-          const Box& b = boxes[id];
-          int bi = static_cast<int>((0.5 * (b.lo[axis] + b.hi[axis]) - cb.lo[axis]) * k1);
-          return std::min(std::max(bi, 0), kBins - 1) < best_split;
+        auto it = std::partition(p.begin() + start, p.begin() + end, [&](const PrimRec& r) {
+          return bin_of(0.5 * (r.lo[axis] + r.hi[axis]), axis) < best_split;
         });
-        mid = it - ids.begin();
+        mid = it - p.begin();
+        for (uint64_t w = occ[axis]; w; w &= w - 1) {
+          const int b = __builtin_ctzll(w);
+          const Bin& bn = bins[axis][b];
+          Box& box = b < best_split ? lb : rb;
+          Box& cbox = b < best_split ? lcb : rcb;
+          box = box_union(box, bn.box);
+          cbox = box_union(cbox, bn.cbox);
+        }
+        child_boxes = true;
       }
     } else if (n <= kMaxLeaf) {
       *count = static_cast<int32_t>(n);
       return leaf(start, n);
     }
     if (mid <= start || mid >= end) {  // degenerate: split by object median on the axis
-      std::nth_element(ids.begin() + start, ids.begin() + start + n / 2, ids.begin() + end,
-                       [&](int64_t a, int64_t b) {
-                         return boxes[a].lo[axis] + boxes[a].hi[axis] <
-                                boxes[b].lo[axis] + boxes[b].hi[axis];
+      std::nth_element(p.begin() + start, p.begin() + start + n / 2, p.begin() + end,
+                       [&](const PrimRec& a, const PrimRec& b) {
+                         return a.lo[axis] + a.hi[axis] < b.lo[axis] + b.hi[axis];
                        });
       mid = start + n / 2;
+      child_boxes = false;
+    }
+    if (!child_boxes) {
+      range_boxes(start, mid, &lb, &lcb);
+      range_boxes(mid, end, &rb, &rcb);
     }
     *count = 0;
     const int32_t node = new_node();
     out.depth = std::max(out.depth, depth);
-    const Box lb = range_box(start, mid);
-    const Box rb = range_box(mid, end);
     int32_t lc = 0, rc = 0;
-    const int32_t l = sah_child(start, mid, lb, depth + 1, &lc);
+    if (parallel && n >= kSpawnMin) {
+      // the two subtrees concurrently, each into its own buffers, then spliced in depth-first order.
+      // Every range above kSpawnMin gets a thread of its own (~2n / kSpawnMin threads in all), so the
+      // OS balances the uneven SAH subtrees over the cores; the data-parallel loops split the budget
+      Bvh lt, rt;
+      SahBuilder lb_{p, lt, std::max(1, threads / 2), kBins, axes, kMaxLeaf, trav_cost, parallel};
+      SahBuilder rb_{p, rt, std::max(1, threads - threads / 2), kBins, axes, kMaxLeaf, trav_cost, parallel};
+      int32_t lcode = 0, rcode = 0;
+      std::thread left_thread([&]() { lcode = lb_.sah_child(start, mid, lb, lcb, depth + 1, &lc); });
+      rcode = rb_.sah_child(mid, end, rb, rcb, depth + 1, &rc);
+      left_thread.join();
+      set_child(node, 0, splice(lt, lcode), lc, lb);
+      set_child(node, 1, splice(rt, rcode), rc, rb);
+      return node;
+    }
+    const int32_t l = sah_child(start, mid, lb, lcb, depth + 1, &lc);
     set_child(node, 0, l, lc, lb);
-    const int32_t r = sah_child(mid, end, rb, depth + 1, &rc);
+    const int32_t r = sah_child(mid, end, rb, rcb, depth + 1, &rc);
     set_child(node, 1, r, rc, rb);
     return node;
+  }
+
+  // Append a subtree built into its own buffers (root code `code`: node 0 of `t`, or a leaf) and
+  // return its code in `out`: node indices shift by the nodes already in `out`, leaf slots by its refs
+  // (the order a single-thread build would have numbered them in).
+  int32_t splice(const Bvh& t, int32_t code) {
+    const int32_t node_off = static_cast<int32_t>(out.nodes.size());
+    const int32_t ref_off = static_cast<int32_t>(out.refs.size());
+    auto fix = [&](int32_t c) {
+      if (c == kEmptyChild) return c;
+      return c >= 0 ? c + node_off : c - ref_off;  // leaf -(1 + slot) -> -(1 + slot + ref_off)
+    };
+    for (BuildNode n : t.nodes) {
+      n.child[0] = fix(n.child[0]);
+      n.child[1] = fix(n.child[1]);
+      out.nodes.push_back(n);
+    }
+    out.refs.insert(out.refs.end(), t.refs.begin(), t.refs.end());
+    out.depth = std::max(out.depth, t.depth);
+    return fix(code);
   }
 };
 
@@ -330,11 +555,19 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
     const Bvh& bin;
     Bvh4* out;
     decltype(slot_of)& slot;
-    std::vector<Slot> gather(int32_t b) {
-      std::vector<Slot> slots;
+    // up to four slots, no heap (the collapse visits every node of a 1M-primitive tree)
+    struct Slots {
+      Slot s[4];
+      size_t n = 0;
+      size_t size() const { return n; }
+      Slot& operator[](size_t i) { return s[i]; }
+      const Slot& operator[](size_t i) const { return s[i]; }
+    };
+    Slots gather(int32_t b) {
+      Slots slots;
       const BuildNode& n = bin.nodes[b];
       for (int side = 0; side < 2; ++side)
-        if (n.child[side] != kEmptyChild) slots.push_back(slot(n, side));
+        if (n.child[side] != kEmptyChild) slots.s[slots.n++] = slot(n, side);
       while (slots.size() < 4) {
         int best = -1;
         double best_area = -1.0;
@@ -348,16 +581,27 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
         }
         if (best < 0) break;
         const BuildNode& c = bin.nodes[slots[best].code];
-        std::vector<Slot> kids;
+        Slot kids[2];
+        size_t nk = 0;
         for (int side = 0; side < 2; ++side)
-          if (c.child[side] != kEmptyChild) kids.push_back(slot(c, side));
-        if (kids.size() + slots.size() - 1 > 4) break;
-        slots.erase(slots.begin() + best);
-        slots.insert(slots.begin() + best, kids.begin(), kids.end());
+          if (c.child[side] != kEmptyChild) kids[nk++] = slot(c, side);
+        if (nk + slots.size() - 1 > 4) break;
+        // replace slot `best` by the kids, in place (the order a vector erase + insert gives)
+        Slot next[4];
+        size_t m = 0;
+        for (size_t i = 0; i < slots.size(); ++i) {
+          if (static_cast<int>(i) == best) {
+            for (size_t k = 0; k < nk; ++k) next[m++] = kids[k];
+          } else {
+            next[m++] = slots[i];
+          }
+        }
+        for (size_t i = 0; i < m; ++i) slots.s[i] = next[i];
+        slots.n = m;
       }
       return slots;
     }
-    std::array<int32_t, 4> children(const std::vector<Slot>& slots, int depth, int pushes) {
+    std::array<int32_t, 4> children(const Slots& slots, int depth, int pushes) {
       out->depth = std::max(out->depth, depth);
       const int here = pushes + static_cast<int>(slots.size()) - 1;
       out->max_pushes = std::max(out->max_pushes, here);
@@ -375,7 +619,7 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
       return codes;
     }
     int32_t fill(int32_t me, int32_t b, int depth, int pushes) {
-      std::vector<Slot> slots = gather(b);
+      const Slots slots = gather(b);
       std::array<int32_t, 4> codes = children(slots, depth, pushes);
       BuildNode4& o = out->nodes[me];
       for (int i = 0; i < 4; ++i) {
@@ -434,13 +678,34 @@ bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
     *err = "too many primitives";
     return false;
   }
-  std::vector<Box> boxes(n);
-  for (int64_t i = 0; i < n; ++i) prim_bbox(desc->prims[i], boxes[i].lo, boxes[i].hi);
-  std::vector<int64_t> ids(n);
-  for (int64_t i = 0; i < n; ++i) ids[i] = i;
+  // RTG_BUILD_THREADS, else the host's threads (at most 16: the GPU box's cgroup quota)
+  int threads = static_cast<int>(std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("RTG_BUILD_THREADS")) threads = std::atoi(e);
+  threads = std::min(16, std::max(1, threads));
   out->nodes.reserve(n * 2);
   out->refs.reserve(n);
-  Builder b{boxes, *out, ids};
+  if (desc->bvh_mode == RTG_BVH_MEDIAN) {
+    std::vector<Box> boxes(n);
+    for (int64_t i = 0; i < n; ++i) prim_bbox(desc->prims[i], boxes[i].lo, boxes[i].hi);
+    std::vector<int64_t> ids(n);
+    for (int64_t i = 0; i < n; ++i) ids[i] = i;
+    Builder b{boxes, *out, ids};
+    b.median(0, n, 1);
+    return true;
+  }
+  if (desc->bvh_mode != RTG_BVH_SAH) {
+    *err = "unknown bvh_mode";
+    return false;
+  }
+  std::vector<PrimRec> recs(n);
+  par_chunks(0, n, n >= SahBuilder::kParMin ? threads : 1, [&](int64_t a, int64_t e, int) {
+    for (int64_t i = a; i < e; ++i) {
+      prim_bbox(desc->prims[i], recs[i].lo, recs[i].hi);
+      recs[i].id = i;
+    }
+  });
+  SahBuilder b{recs, *out, threads};
+  b.parallel = threads > 1;
   // RTG_SAH_TUNE="trav_cost:max_leaf[:axes[:bins]]" overrides the SAH constants (tuning experiments only)
   if (const char* tune = std::getenv("RTG_SAH_TUNE")) {
     double ct = 0.0;
@@ -449,24 +714,17 @@ bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
       b.trav_cost = ct;
       b.kMaxLeaf = ml;
       b.axes = ax == 3 ? 3 : 1;
-      b.kBins = std::min(std::max(nb, 2), int(Builder::kMaxBins));
+      b.kBins = std::min(std::max(nb, 2), int(SahBuilder::kMaxBins));
     }
   }
-  if (desc->bvh_mode == RTG_BVH_MEDIAN) {
-    b.median(0, n, 1);
-  } else if (desc->bvh_mode == RTG_BVH_SAH) {
-    Box all;
-    for (int64_t i = 0; i < n; ++i) all = box_union(all, boxes[i]);
-    int32_t cnt = 0;
-    const int32_t code = b.sah_child(0, n, all, 1, &cnt);
-    if (code < 0) {  // the whole scene is one leaf: wrap it into a root node
-      const int32_t root = b.new_node();
-      out->depth = 1;
-      b.set_child(root, 0, code, cnt, all);
-    }
-  } else {
-    *err = "unknown bvh_mode";
-    return false;
+  Box all, cb;
+  b.range_boxes(0, n, &all, &cb);
+  int32_t cnt = 0;
+  const int32_t code = b.sah_child(0, n, all, cb, 1, &cnt);
+  if (code < 0) {  // the whole scene is one leaf: wrap it into a root node
+    const int32_t root = b.new_node();
+    out->depth = 1;
+    b.set_child(root, 0, code, cnt, all);
   }
   return true;
 }

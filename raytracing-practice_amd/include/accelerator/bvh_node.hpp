@@ -6,6 +6,8 @@
 // the flat scene lists objects exactly as the reference's hittable_list did.
 #pragma once
 #include <algorithm>
+#include <atomic>
+#include <mutex>
 
 #include "accelerator/aabb.hpp"
 #include "hittable/hittable.hpp"
@@ -13,21 +15,34 @@
 
 class bvh_node : public hittable {
  public:
-  bvh_node(hittable_list list) : bvh_node(list.objects, 0, list.objects.size(), list.objects) {}
+  // The root over a whole list (main.cpp:76). The reference builds the tree here; the mirror keeps
+  // the list in insertion order, computes the root box (a union: order-independent, the same box) and
+  // builds the host-side children only on the first host hit(): a render flattens the list and the
+  // device builds its own BVH, so it never needs them, and config 5's 1M-sphere scene no longer pays
+  // the reference's median build (4.2 s) before every upload.
+  bvh_node(hittable_list list) : list_order(std::move(list.objects)) {
+    bbox = aabb::empty;
+    for (const auto& o : list_order) bbox = aabb(bbox, o->bounding_box());
+  }
 
+  // bvh_node.hpp:25-77 as the reference has it (sorts `objects` in place, builds eagerly)
   bvh_node(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end) {
     build(objects, start, end);
+    built_ = true;
   }
 
  private:
-  // root only: the unsorted object list, in insertion order
-  bvh_node(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end,
-           std::vector<std::shared_ptr<hittable>> original)
-      : list_order(std::move(original)) {
-    build(objects, start, end);
+  void ensure_built() const {
+    std::call_once(once_, [this]() {
+      if (built_) return;
+      std::vector<std::shared_ptr<hittable>> objects(list_order);
+      const_cast<bvh_node*>(this)->build(objects, 0, objects.size());
+      built_ = true;
+    });
   }
 
   void build(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end) {
+    if (start >= end) return;  // an empty list: no children, every ray misses the empty box
     bbox = aabb::empty;
     for (size_t i = start; i < end; ++i) bbox = aabb(bbox, objects[i]->bounding_box());
     const int axis = bbox.longest_axis();
@@ -50,7 +65,8 @@ class bvh_node : public hittable {
 
  public:
   bool hit(const ray& r, interval ray_t, hit_record& rec) const override {
-    if (!bbox.hit(r, ray_t)) return false;
+    if (!built_) ensure_built();
+    if (!left || !bbox.hit(r, ray_t)) return false;
     const bool hl = left->hit(r, ray_t, rec);
     const bool hr = right->hit(r, interval(ray_t.min, hl ? rec.t : ray_t.max), rec);
     return hl || hr;
@@ -59,6 +75,7 @@ class bvh_node : public hittable {
 
   bool rtg_flatten(rtgpu::scene_builder& sb, const vec3& offset) const override {
     if (!list_order.empty()) {
+      sb.reserve(list_order.size());
       for (const auto& obj : list_order)
         if (!obj->rtg_flatten(sb, offset)) return false;
       return true;
@@ -71,4 +88,6 @@ class bvh_node : public hittable {
   std::vector<std::shared_ptr<hittable>> list_order;
   std::shared_ptr<hittable> left, right;
   aabb bbox;
+  mutable std::once_flag once_;
+  mutable std::atomic<bool> built_{false};
 };

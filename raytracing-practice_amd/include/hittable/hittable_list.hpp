@@ -3,6 +3,7 @@
 #include <vector>
 
 #include "hittable/hittable.hpp"
+#include "rtgpu/scene_builder.hpp"
 
 class hittable_list : public hittable {
  public:
@@ -32,6 +33,7 @@ class hittable_list : public hittable {
   }
   aabb bounding_box() const override { return bbox; }
   bool rtg_flatten(rtgpu::scene_builder& sb, const vec3& offset) const override {
+    sb.reserve(objects.size());
     for (const auto& obj : objects)
       if (!obj->rtg_flatten(sb, offset)) return false;
     return true;

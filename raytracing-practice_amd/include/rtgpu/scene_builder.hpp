@@ -4,7 +4,7 @@
 // texture shared by many spheres (e.g. main.cpp:180-183) is uploaded once.
 #pragma once
 #include <cstdint>
-#include <map>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -47,12 +47,22 @@ class scene_builder {
     perlins.push_back(p);
     return memo[key] = static_cast<int32_t>(perlins.size() - 1);
   }
+  // Capacity for `n` more objects (each may bring a material and a texture of its own, as config 5's
+  // 1M spheres do): one allocation per array and no rehashing while a large list flattens.
+  void reserve(size_t n) {
+    if (n < 1024) return;
+    prims.reserve(prims.size() + n);
+    materials.reserve(materials.size() + n);
+    textures.reserve(textures.size() + n);
+    memo_[kMaterial].reserve(memo_[kMaterial].size() + n);
+    memo_[kTexture].reserve(memo_[kTexture].size() + n);
+  }
   bool fail(const std::string& what) {
     if (error.empty()) error = what;
     return false;
   }
-  // identity -> index table, one per exported object kind
-  std::map<const void*, int32_t>& memo_table(memo_kind k) { return memo_[k]; }
+  // identity -> index table, one per exported object kind (hashed: config 5 flattens 1M materials)
+  std::unordered_map<const void*, int32_t>& memo_table(memo_kind k) { return memo_[k]; }
 
   rtg_scene_desc desc(int32_t bvh_mode) const {
     rtg_scene_desc d{};
@@ -72,7 +82,7 @@ class scene_builder {
   }
 
  private:
-  std::map<const void*, int32_t> memo_[4];
+  std::unordered_map<const void*, int32_t> memo_[4];
 };
 
 }  // namespace rtgpu

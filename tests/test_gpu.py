@@ -99,7 +99,7 @@ def test_depth100_scenes_match_oracle(gpu_lib, scenes, oracle, name, W, spp):
 # (tests/golden/moments_*.npz, >= 2048 samples per pixel of the ref-hybrid render from glibc rand()
 # streams). GPU samples per pixel: enough that 8x8-block means are gaussian.
 G5_GPU = [("book1", 1024), ("cornell", 2048), ("cornell_translate", 2048), ("simple_light", 1024),
-          ("perlin", 1024), ("book1_g500", 1024)]
+          ("perlin", 1024), ("book1_g500", 1024), ("earth_perlin", 1024), ("earth", 1024)]
 
 
 @pytest.mark.parametrize("scene,spp", G5_GPU)
@@ -786,6 +786,35 @@ def test_render_plan_names_the_kernel(gpu_lib, scenes, name, grid, W, schedule, 
     assert (p.schedule, p.dual, p.waves_per_simd) == (schedule, dual, waves_per_simd), p.as_dict()
     assert 0 < p.vgprs <= 512 // waves_per_simd and p.chunks == 32 and p.chunk_samples == 16
     assert p.num_cus > 0 and p.workgroups > 0
+
+
+def test_bench_two_ranks_rehearsal(tmp_path):
+    """bench.py's N > 1 flow (interleaved shards, the gather on rank 0, per-rank records, the per-pixel
+    check of the gathered frame against cpu_ref32, max-over-ranks timing) with two ranks on this one GPU
+    over gloo (RCCL takes one rank per device, so the rtg_gather_rows cross-check is the driver's
+    multi-GPU run's). The gathered frame must match the oracle on the sampled rows."""
+    import json
+    import socket
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--dist-backend", "gloo", "--width", "192", "--height", "108", "--spp", "8",
+           "--depth", "10", "--steps", "2", "--warmup", "1", "--parity-seconds", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and [x["rank"] for x in line["ranks"]] == [0, 1]
+    assert [x["rows"] for x in line["ranks"]] == [54, 54] and all(x["segments"] > 0 for x in line["ranks"])
+    assert line["parity"]["pass"] and line["parity"]["rows"] >= 2, line["parity"]
+    assert line["parity"]["identical_frac"] > 0.999
+    assert all(g is not None and g >= 0 for g in line["gather_ms"])
+    assert line["cpu_baseline"] is None  # rank 0 at N = 1 only
 
 
 def test_numerics_helpers_match_ieee():

@@ -297,3 +297,28 @@ def test_write_color_bytes_matches_oracle(oracle):
     got = rtgpu.write_color_bytes(vals.reshape(-1, 1).repeat(3, axis=1))[:, 0]
     want = [oracle.write_color([float(v)] * 3)[0] for v in vals]
     assert np.array_equal(got.astype(int), np.array(want))
+
+
+def test_parallel_sah_build_is_the_single_thread_tree(lib, scenes, monkeypatch):
+    """The host SAH builder runs its top-level loops and large subtrees on several threads (config 5's
+    setup, DESIGN.md §3 "BVH"): bins merge by exact min / max and counts, the partitions stay
+    sequential and subtrees are spliced in depth-first order, so the tree (nodes, boxes, leaf refs)
+    must be the single-thread build's, bit for bit. 90k spheres: subtrees above 32k primitives spawn,
+    loops above 64k run data-parallel."""
+    import ctypes as C
+
+    s = scenes.build("bouncing_spheres", grid=150, rand_seed=1)
+    d = rtgpu.rtg_scene_desc.from_buffer_copy(s.desc)
+    d.bvh_mode = rtgpu.RTG_BVH_SAH
+    trees = {}
+    for t in ("1", "8"):
+        monkeypatch.setenv("RTG_BUILD_THREADS", t)
+        nn, nr, depth = C.c_int64(0), C.c_int64(0), C.c_int32(0)
+        lib.check("rtg_bvh_build_host", lib.lib.rtg_bvh_build_host(
+            C.byref(d), None, 0, None, 0, C.byref(nn), C.byref(nr), C.byref(depth)))
+        nodes = (rtgpu.rtg_bvh_node_host * nn.value)()
+        refs = (C.c_int64 * nr.value)()
+        lib.check("rtg_bvh_build_host", lib.lib.rtg_bvh_build_host(
+            C.byref(d), nodes, nn.value, refs, nr.value, C.byref(nn), C.byref(nr), C.byref(depth)))
+        trees[t] = (bytes(nodes), bytes(refs), depth.value)
+    assert nn.value > 40000 and trees["1"] == trees["8"]

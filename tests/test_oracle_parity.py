@@ -17,7 +17,8 @@ import rtgpu
 from conftest import GOLDEN
 
 SCENE_OF = {"book1": "bouncing_spheres", "cornell": "cornell_box", "simple_light": "simple_light",
-            "perlin": "perlin_sphere", "cornell_translate": "cornell_translate"}
+            "perlin": "perlin_sphere", "cornell_translate": "cornell_translate", "earth": "earth",
+            "earth_perlin": "earth_perlin"}
 
 
 def hybrid_camera(scene, W, H, spp, depth):
@@ -32,6 +33,8 @@ def hybrid_camera(scene, W, H, spp, depth):
         kw.update(background=(0, 0, 0), vfov=40.0, lookfrom=(278, 278, -800), lookat=(278, 278, 0))
     elif scene == "simple_light":
         kw.update(background=(0, 0, 0), lookfrom=(26, 3, 6), lookat=(0, 2, 0))
+    elif scene == "earth":
+        kw.update(lookfrom=(0, 0, 12))
     return rtgpu.camera(**kw)
 
 

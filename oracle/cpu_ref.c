@@ -858,7 +858,9 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   if (disc < 0.0f) return -1.0f;
   float sq = sqrtf(disc);
   float q = -(hb + copysignf(sq, hb));
-  if (q == 0.0f || a == 0.0f) return -1.0f;
+  /* |q| < 2^-100 (a ray tangent at its own origin) counts as a miss: the rtg-f32 spec's guard that
+     keeps the device's division (div_rn, no special-case steps) in range */
+  if (fabsf(q) < 0x1p-100f || a == 0.0f) return -1.0f;
   float t0 = q * inv_a, t1 = c / q; /* far root by the reciprocal, near root divided */
   float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
   if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;

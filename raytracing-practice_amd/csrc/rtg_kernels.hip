@@ -159,9 +159,13 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   if (disc < 0.0f) return -1.0f;
   const float sq = sqrtf(disc);
   const float q = -(hb + copysignf(sq, hb));
-  if (q == 0.0f || a == 0.0f) return -1.0f;
+  // |q| < 2^-100 (a ray tangent at its own origin, q would otherwise have no lower bound) counts as a
+  // miss in the rtg-f32 spec (oracle/cpu_ref.c the same): div_rn is exact for every divisor left, and
+  // the guard is the compare the q == 0 test already made (div_rn_wide, which scaled tiny
+  // divisors instead, cost earth_perlin 4-6 % in register allocation, profiles/r03_c/ab_div_*)
+  if (fabsf(q) < 0x1p-100f || a == 0.0f) return -1.0f;
   const float t0 = q * inv_a;
-  const float t1 = div_rn_wide(c, q);  // q has no lower bound (tangent rays): ADVICE r02
+  const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
   if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
@@ -654,23 +658,44 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
   const float uu = u * u * (3.0f - 2.0f * u);
   const float vv = v * v * (3.0f - 2.0f * v);
   const float ww = w * w * (3.0f - 2.0f * w);
-  // the six permutation entries, then all eight corner gradients, are fetched before any of them is
-  // used: one LDS round trip each instead of eight dependent ones per octave (config 3 shades 7
-  // octaves per ground hit); the sum below keeps the reference's corner order
+  // the six permutation entries are fetched before any of them is used (round 2: one LDS round trip
+  // instead of dependent ones per octave; config 3 shades 7 octaves per ground hit)
   const int px[2] = {perm[i & 255], perm[(i + 1) & 255]};
   const int py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
   const int pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
+  float accum = 0.0f;
+#ifdef RTG_AB_PERLIN8  // A/B only: round 2's eight float4 gradients fetched at once
   float4 g[8];
 #pragma unroll
   for (int c = 0; c < 8; ++c) g[c] = vec[px[c >> 2] ^ py[(c >> 1) & 1] ^ pz[c & 1]];
-  float accum = 0.0f;
+#pragma unroll
+  for (int di = 0; di < 2; ++di)
+#pragma unroll
+    for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+      for (int dk = 0; dk < 2; ++dk) {
+        const V3 c = xyz(g[di * 4 + dj * 2 + dk]);
+        const V3 wv = v3(u - di, v - dj, w - dk);
+        const float fu = di ? uu : (1.0f - uu);
+        const float fv = dj ? vv : (1.0f - vv);
+        const float fw = dk ? ww : (1.0f - ww);
+        accum = fmaf(fu * fv * fw, dot(c, wv), accum);
+      }
+  return accum;
+#endif
+  // the corner gradients in pairs (di, dj fixed; dk = 0, 1), each pair fetched (xyz only) before it
+  // is used and the sum in the reference's corner order: fetching all eight float4s at once (round 2)
+  // saved LDS round trips but made the textured kernel spill its path state to scratch at 5 waves
+  // per SIMD (config 3: 97 GB of scratch write traffic per frame, TA 69 % busy, profiles/r03_c)
 #pragma unroll
   for (int di = 0; di < 2; ++di) {
 #pragma unroll
     for (int dj = 0; dj < 2; ++dj) {
+      const int pij = px[di] ^ py[dj];
+      const V3 g0 = xyz(vec[pij ^ pz[0]]), g1 = xyz(vec[pij ^ pz[1]]);
 #pragma unroll
       for (int dk = 0; dk < 2; ++dk) {
-        const V3 c = xyz(g[di * 4 + dj * 2 + dk]);
+        const V3 c = dk ? g1 : g0;
         const V3 wv = v3(u - di, v - dj, w - dk);
         const float fu = di ? uu : (1.0f - uu);
         const float fv = dj ? vv : (1.0f - vv);

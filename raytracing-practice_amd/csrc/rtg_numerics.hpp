@@ -24,14 +24,6 @@ __device__ __forceinline__ float div_rn(float x, float y) {
   const float e2 = fmaf(-y, q1, x);
   return fmaf(e2, r, q1);
 }
-// div_rn for divisors with no lower bound (the sphere test's near root c / q: q = -(h +- sqrt(disc))
-// approaches 0 for a ray tangent at its own origin): below 2^-60 both operands are scaled by 2^64
-// first, an exact power-of-two scaling, so the quotient is the same correctly rounded value; covers
-// |y| down to the smallest denormal for |x| <= 2^60 and quotients below 2^126 (4 VALU more).
-__device__ __forceinline__ float div_rn_wide(float x, float y) {
-  const float s = fabsf(y) < 0x1p-60f ? 0x1p64f : 1.0f;
-  return div_rn(x * s, y * s);
-}
 // sqrt_rn: the compiler's correctly rounded sqrt (v_sqrt_f32, then the neighbour whose residual
 // changes sign) without its 2^32 pre-scaling of x < 2^-96 and its 0/inf class fix-up: exact for x
 // == 0 and 2^-96 <= x < inf, 9 VALU instead of 16. Call sites: 1 - z^2 of a 24-bit uniform, a

@@ -27,8 +27,8 @@ __device__ __forceinline__ float rand_float(uint64_t h, int emin, int emax) {
 }
 
 // out[0] division mismatches, out[1] sqrt mismatches (random operands), out[2] sqrt mismatches on
-// the kernel's 1 - z^2 / uniform operands, out[3] operands tested, out[4] div_rn_wide mismatches on
-// tiny divisors (2^-149 .. 2^-20, denormals included); ex[0..3] the last mismatch seen
+// the kernel's 1 - z^2 / uniform operands, out[3] operands tested, out[4] div_rn mismatches on the
+// sphere test's small divisors (2^-100 .. 2^-20); ex[0..3] the last mismatch seen
 __global__ void check_kernel(uint64_t n, uint64_t seed, unsigned long long* out, float* ex) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   unsigned long long bad_div = 0, bad_sqrt = 0, bad_kern = 0, bad_wide = 0;
@@ -46,21 +46,17 @@ __global__ void check_kernel(uint64_t n, uint64_t seed, unsigned long long* out,
       ++bad_div;
       ex[0] = x, ex[1] = y;
     }
-    // the sphere test's near root c / q (div_rn_wide): numerators 2^-60 .. 2^40, divisors 2^-126 ..
-    // 2^-20 and denormal ones (1/16 of them), quotients below 2^120 (the kernel's c / q is a
+    // the sphere test's near root c / q with the spec's guard (|q| >= 2^-100 reaches the division):
+    // numerators 2^-60 .. 2^40, divisors 2^-100 .. 2^-20, quotients below 2^120 (c / q is a
     // distance compared with tmin and the closest hit)
     {
       const float xw = (h2 & 63) == 3 ? 0.0f : rand_float(h3, -60, 40);
-      float yw = rand_float(h0 ^ h1, -126, -20);
-      if (((h1 >> 40) & 15) == 0)  // a denormal divisor
-        yw = __uint_as_float((static_cast<uint32_t>(h0 >> 40) & 0x7fffffu) | 1u | (static_cast<uint32_t>(h1 >> 63) << 31));
+      const float yw = rand_float(h0 ^ h1, -100, -20);
       const float qi = xw / yw;
-      if (fabsf(qi) < 0x1p120f && __float_as_uint(rtg::div_rn_wide(xw, yw)) != __float_as_uint(qi)) {
+      if (fabsf(qi) < 0x1p120f && __float_as_uint(rtg::div_rn(xw, yw)) != __float_as_uint(qi)) {
         ++bad_wide;
         ex[0] = xw, ex[1] = yw;
       }
-      // the common range goes through the unscaled path unchanged
-      if (__float_as_uint(rtg::div_rn_wide(x, y)) != __float_as_uint(q_ieee)) ++bad_wide;
     }
     // square root: 0 and 2^-90 .. 2^100
     float s = fabsf(rand_float(h3, -90, 100));

@@ -822,9 +822,9 @@ def test_numerics_helpers_match_ieee():
     rounded `x / y` and `sqrtf` on 2^24 random operands of each kind from the ranges the kernels use:
     numerators 2^-60..2^61 (with zeros and ones), divisors 2^-30..2^31, sqrt operands 0 and
     2^-90..2^101, and the kernels' own sqrt operands (a 24-bit uniform U, 1 - z^2 for z = 1 - 2U,
-    plain and fused); and div_rn_wide, the sphere test's near-root division, on divisors down to
-    the denormals (2^-149 .. 2^-20) with numerators 2^-60..2^40 (tangent rays make that
-    divisor arbitrarily small)."""
+    plain and fused); and the sphere test's near-root division c / q on the small divisors its guard
+    lets through (2^-100 .. 2^-20, numerators 2^-60..2^40; ADVICE r02: tangent rays make q arbitrarily
+    small, and |q| < 2^-100 is a miss in the spec)."""
     import ctypes as C
     so = C.CDLL(os.path.join(REPO, "tests", "native", "libnumcheck.so"))
     so.rtg_numerics_check.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_ulonglong), C.POINTER(C.c_float)]

@@ -531,11 +531,126 @@ void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]) {
   }
 }
 
-void collapse_bvh4(const Bvh& bin, Bvh4* out) {
+// SAH-optimal 4-wide collapse (the dynamic program of Ylitie, Karras and Laine, "Efficient
+// Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs", HPG 2017, for width 4): for every
+// binary subtree and every budget i = 1..4 of slots it may occupy under a wide parent, the cheapest
+// representation by surface-area cost — one slot that is a merged leaf (its primitives are a
+// contiguous ref range, <= max_leaf of them) or a wide node, or its two children sharing the budget.
+// cost(wide node) = area x c_node + its slots; cost(leaf) = area x count x 1.
+struct CollapseDp {
+  const Bvh& bin;
+  double c_node;
+  int max_leaf;
+  std::vector<double> cost;   // [node][i], i = 0..3 for budgets 1..4
+  std::vector<int8_t> pick;   // [node][i]: -1 = budget i-1 (i > 0), 0 = one slot, k = k slots to the left child
+  std::vector<uint8_t> as_leaf;  // budget 1: merged leaf (1) or wide node (0)
+  std::vector<int8_t> wide_k;    // slots of the left child when the node is a wide node (d[4])
+  std::vector<int64_t> first, count;
+  std::vector<Box> box;
+
+  struct SlotRef {  // a child slot of a binary node: an inner node or a leaf range
+    int32_t code, cnt;
+    Box b;
+  };
+  SlotRef slot_of(int32_t node, int side) const {
+    const BuildNode& n = bin.nodes[node];
+    SlotRef s;
+    s.code = n.child[side];
+    s.cnt = n.count[side];
+    for (int k = 0; k < 3; ++k) {
+      s.b.lo[k] = n.lo[side][k];
+      s.b.hi[k] = n.hi[side][k];
+    }
+    return s;
+  }
+  double slot_cost(const SlotRef& s, int i) const {  // budget i (1..4)
+    if (s.code < 0) return half_area(s.b) * s.cnt;
+    return cost[static_cast<size_t>(s.code) * 4 + (i - 1)];
+  }
+
+  void run() {
+    const size_t n = bin.nodes.size();
+    cost.assign(n * 4, 0.0);
+    pick.assign(n * 4, 0);
+    as_leaf.assign(n, 0);
+    wide_k.assign(n, 0);
+    first.assign(n, 0);
+    count.assign(n, 0);
+    box.assign(n, Box{});
+    // node boxes from the parents' child slots (children follow their parent in depth-first order)
+    box[0] = box_union(slot_of(0, 0).b, bin.nodes[0].child[1] != kEmptyChild ? slot_of(0, 1).b : Box{});
+    for (size_t m = 0; m < n; ++m)
+      for (int side = 0; side < 2; ++side) {
+        const SlotRef s = slot_of(static_cast<int32_t>(m), side);
+        if (s.code >= 0) box[s.code] = s.b;
+      }
+    for (size_t mm = n; mm-- > 0;) {
+      const int32_t m = static_cast<int32_t>(mm);
+      const BuildNode& nd = bin.nodes[m];
+      int64_t f = INT64_MAX, c = 0;
+      for (int side = 0; side < 2; ++side) {
+        if (nd.child[side] == kEmptyChild) continue;
+        const SlotRef s = slot_of(m, side);
+        if (s.code < 0) {
+          f = std::min<int64_t>(f, -(static_cast<int64_t>(s.code) + 1));
+          c += s.cnt;
+        } else {
+          f = std::min(f, first[s.code]);
+          c += count[s.code];
+        }
+      }
+      first[m] = f;
+      count[m] = c;
+      const bool two = nd.child[1] != kEmptyChild;
+      const SlotRef l = slot_of(m, 0);
+      const SlotRef r = two ? slot_of(m, 1) : SlotRef{};
+      double d[5];  // d[j]: the two children sharing j slots
+      int dk[5];
+      for (int j = 1; j <= 4; ++j) {
+        d[j] = kInf;
+        dk[j] = 0;
+        if (!two) {  // a single child: it takes the whole budget
+          d[j] = slot_cost(l, j);
+          dk[j] = j;
+          continue;
+        }
+        for (int k = 1; k < j; ++k) {
+          const double v = slot_cost(l, k) + slot_cost(r, j - k);
+          if (v < d[j]) {
+            d[j] = v;
+            dk[j] = k;
+          }
+        }
+      }
+      const double a = half_area(box[m]);
+      const double c_leaf = c <= max_leaf ? a * static_cast<double>(c) : kInf;
+      const double c_int = a * c_node + d[4];
+      double* cm = &cost[static_cast<size_t>(m) * 4];
+      int8_t* pm = &pick[static_cast<size_t>(m) * 4];
+      as_leaf[m] = c_leaf <= c_int;
+      cm[0] = std::min(c_leaf, c_int);
+      pm[0] = 0;
+      for (int i = 2; i <= 4; ++i) {
+        if (d[i] < cm[i - 2]) {
+          cm[i - 1] = d[i];
+          pm[i - 1] = static_cast<int8_t>(dk[i]);
+        } else {
+          cm[i - 1] = cm[i - 2];
+          pm[i - 1] = -1;
+        }
+      }
+      wide_k[m] = static_cast<int8_t>(dk[4]);  // m as a wide node: its children share four slots so
+    }
+  }
+};
+
+void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
   out->nodes.clear();
   out->depth = 0;
   out->max_pushes = 0;
   if (bin.nodes.empty()) return;
+  CollapseDp dp{bin, prm.c_node, prm.max_leaf, {}, {}, {}, {}, {}, {}, {}};
+  if (prm.sah) dp.run();
   struct Slot {
     int32_t code, count;
     Box box;
@@ -555,6 +670,7 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
     const Bvh& bin;
     Bvh4* out;
     decltype(slot_of)& slot;
+    const CollapseDp* dp;  // SAH-optimal collapse, or null: greedy (open the largest-area inner child)
     // up to four slots, no heap (the collapse visits every node of a 1M-primitive tree)
     struct Slots {
       Slot s[4];
@@ -563,9 +679,56 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
       Slot& operator[](size_t i) { return s[i]; }
       const Slot& operator[](size_t i) const { return s[i]; }
     };
+    // the DP's slots of wide node b: its children sharing four slots as the program chose
+    void expand(Slots& out_slots, int32_t node, int side, int budget) const {
+      const CollapseDp::SlotRef s = dp->slot_of(node, side);
+      if (s.code < 0) {  // a leaf of the binary tree stays a leaf
+        Slot sl;
+        sl.code = s.code;
+        sl.count = s.cnt;
+        sl.box = s.b;
+        out_slots.s[out_slots.n++] = sl;
+        return;
+      }
+      expand_node(out_slots, s.code, budget);
+    }
+    void expand_node(Slots& out_slots, int32_t m, int budget) const {
+      const int8_t* pm = &dp->pick[static_cast<size_t>(m) * 4];
+      while (budget > 1 && pm[budget - 1] == -1) --budget;
+      if (budget == 1) {
+        Slot sl;
+        sl.box = dp->box[m];
+        if (dp->as_leaf[m]) {  // merged leaf: the subtree's contiguous refs
+          sl.code = -(1 + static_cast<int32_t>(dp->first[m]));
+          sl.count = static_cast<int32_t>(dp->count[m]);
+        } else {
+          sl.code = m;
+          sl.count = 0;
+        }
+        out_slots.s[out_slots.n++] = sl;
+        return;
+      }
+      const int k = pm[budget - 1];
+      if (bin.nodes[m].child[1] == kEmptyChild) {
+        expand(out_slots, m, 0, budget);
+        return;
+      }
+      expand(out_slots, m, 0, k);
+      expand(out_slots, m, 1, budget - k);
+    }
     Slots gather(int32_t b) {
       Slots slots;
       const BuildNode& n = bin.nodes[b];
+      if (dp) {  // b is a wide node: its two children share the four slots
+        const int k = dp->wide_k[b];
+        if (n.child[1] == kEmptyChild) {
+          expand(slots, b, 0, 4);
+        } else {
+          expand(slots, b, 0, k);
+          expand(slots, b, 1, 4 - k);
+        }
+        return slots;
+      }
       for (int side = 0; side < 2; ++side)
         if (n.child[side] != kEmptyChild) slots.s[slots.n++] = slot(n, side);
       while (slots.size() < 4) {
@@ -632,7 +795,7 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out) {
       }
       return me;
     }
-  } rec{bin, out, slot_of};
+  } rec{bin, out, slot_of, prm.sah ? &dp : nullptr};
   out->nodes.push_back(BuildNode4{});  // the root is node 0
   rec.fill(0, 0, 1, 0);
 }

@@ -75,9 +75,15 @@ struct Bvh4 {
   int32_t max_pushes = 0;  // most stack entries an ordered traversal can hold at once
 };
 
-// Collapse a binary child-pair BVH into a 4-wide one (greedy: open the largest-area inner child
-// until four slots are filled); leaf codes and refs are unchanged.
-void collapse_bvh4(const Bvh& bin, Bvh4* out);
+// Collapse a binary child-pair BVH into a 4-wide one: greedy (open the largest-area inner child until
+// four slots are filled; leaves unchanged) or SAH-optimal (dynamic program over the binary tree; may
+// merge small subtrees into leaves of up to max_leaf primitives, whose refs are contiguous).
+struct CollapseParams {
+  bool sah = false;
+  double c_node = 1.0;  // cost of a wide-node visit relative to one primitive test
+  int max_leaf = 4;     // <= 8 (the leaf code's count field)
+};
+void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm = CollapseParams{});
 
 // Renumber a 4-wide tree so its first `top` nodes are the top of the tree in breadth-first order
 // (the root stays node 0; the rest keep their depth-first order). Scenes too large for LDS keep

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--scene", default="bouncing_spheres")
     ap.add_argument("--bvh", default="sah")
     ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--count", action="store_true", help="also report box / prim tests per segment per variant")
+    ap.add_argument("--height", type=int, default=0, help="0: 16:9 of --width")
     a = ap.parse_args()
     import torch
 
@@ -47,22 +49,23 @@ def main():
         libs["lib"] = rtgpu.Library()
     first = next(iter(libs))
     bvh = {"sah": rtgpu.RTG_BVH_SAH, "median": rtgpu.RTG_BVH_MEDIAN, "sah2": 2, "gpu": 3}[a.bvh]
-    s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
+    s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width,
+                                   aspect_ratio=(a.width / a.height) if a.height else 16.0 / 9.0,
                                    spp=a.spp, max_depth=a.depth, bvh_mode=bvh)
     cam = s.camera
     H = libs[first].camera_resolve(cam).image_height
     scenes = {}
 
-    def scene_for(name, tune):
+    def scene_for(name, tune, env=""):
         tune = tune.split("%", 1)[0]
-        if (name, tune) not in scenes:
+        if (name, tune, env) not in scenes:
             if tune.split("@", 1)[0]:
                 os.environ["RTG_SAH_TUNE"] = tune.split("@", 1)[0]
             else:
                 os.environ.pop("RTG_SAH_TUNE", None)
-            scenes[(name, tune)] = libs[name].scene_create(s.desc)
+            scenes[(name, tune, env)] = libs[name].scene_create(s.desc)
             os.environ.pop("RTG_SAH_TUNE", None)
-        return scenes[(name, tune)]
+        return scenes[(name, tune, env)]
     out = torch.zeros((H, a.width, 3), device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -77,13 +80,13 @@ def main():
         variants.append((name, nums, tune, env))
         envs[variants[-1]] = dict(kv.split("=", 1) for kv in env.split(";") if kv)
     times = {v: [] for v in variants}
-    frames, segs = {}, {}
+    frames, segs, counts = {}, {}, {}
     for r in range(a.rounds):
         for v in variants:
-            name, (sched, batch, leaf), tune, _ = v
+            name, (sched, batch, leaf), tune, env = v
             for k, val in envs[v].items():
                 os.environ[k] = val
-            L, ds = libs[name], scene_for(name, tune)
+            L, ds = libs[name], scene_for(name, tune, env)
             if "%" in tune:  # "...%v": RTG_COMBINE=v
                 os.environ["RTG_COMBINE"] = tune.split("%", 1)[1]
                 tune = tune.split("%", 1)[0]
@@ -104,6 +107,16 @@ def main():
             segs[v] = st.segments
             if r == 0:
                 frames[v] = out.cpu().numpy().copy()
+                if a.count:  # box / primitive tests per segment of this variant (counting kernel)
+                    job = rtgpu.rtg_render_desc(0x5EED, 0, 1, 0, flags | rtgpu.RTG_RENDER_COUNT, stream)
+                    cst = rtgpu.rtg_render_stats()
+                    for k2, val in envs[v].items():
+                        os.environ[k2] = val
+                    L.check("rtg_render", L.lib.rtg_render(ds.handle, rtgpu.C.byref(cam), rtgpu.C.byref(job),
+                                                            out.data_ptr(), rtgpu.C.byref(cst)))
+                    for k2 in envs[v]:
+                        os.environ.pop(k2, None)
+                    counts[v] = (cst.box_tests / max(cst.segments, 1), cst.prim_tests / max(cst.segments, 1))
     base = frames[variants[0]]
     res = {}
     for v in variants:
@@ -113,6 +126,9 @@ def main():
                     "mrays_per_s": round(segs[v] / med / 1e3, 1), "segments": int(segs[v]),
                     "identical_frame": bool(np.array_equal(frames[v], base)),
                     "equal_pixel_frac": float(np.mean(np.all(frames[v] == base, axis=-1)))}
+        if v in counts:
+            res[key]["box_tests_per_segment"] = round(counts[v][0], 3)
+            res[key]["prim_tests_per_segment"] = round(counts[v][1], 3)
     for ds in scenes.values():
         ds.close()
     print(json.dumps({"scene": a.scene, "grid": a.grid, "spp": a.spp, "width": a.width, "depth": a.depth,

@@ -408,7 +408,9 @@ def main():
                 f"chunk={rtgpu.chunk_samples(args.spp)}")
     traffic = pmc_traffic(workload) if world == 1 else None
     setup_ms = {"scene_build_ms": round(t_scene * 1e3, 1), "scene_create_ms": round(t_create * 1e3, 1),
-                "bvh_build_ms": round(info.build_ms, 1), "upload_ms": round(info.upload_ms, 1)}
+                "host_compile_ms": round(info.build_ms, 1), "bvh_ms": round(info.bvh_ms, 1),
+                "collapse_ms": round(info.collapse_ms, 1), "flatten_ms": round(info.flatten_ms, 1),
+                "upload_ms": round(info.upload_ms, 1)}
     my = {"rank": rank, "device": local, "rows": n, "row_begin": b, "row_stride": stride,
           "segments": int(segs), "kernel_ms": round(sum(kernel_ms) / len(kernel_ms), 3),
           "kernel_ms_max": round(max(kernel_ms), 3),

@@ -235,6 +235,12 @@ typedef struct rtg_scene_info {
   int64_t device_bytes;
   double build_ms; /* host BVH build + flatten */
   double upload_ms;
+  /* phases of build_ms (ABI 5): binned-SAH build of the binary tree, its 4-wide collapse (+ the
+   * breadth-first renumbering of the tree's top), and the rest (validation, primitive / node /
+   * material / texture records) */
+  double bvh_ms;
+  double collapse_ms;
+  double flatten_ms;
 } rtg_scene_info;
 
 /* Library identity. */

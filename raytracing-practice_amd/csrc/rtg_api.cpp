@@ -5,6 +5,7 @@
 // the gfx950 render kernel (rtg_kernels.hip) on the caller's stream. No CPU fallback exists:
 // without a usable device every entry point that renders returns RTG_E_NODEVICE / RTG_E_HIP.
 #include <algorithm>
+#include <array>
 #include <functional>
 #include <chrono>
 #include <cmath>
@@ -13,6 +14,8 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "rtg_internal.hpp"
 
@@ -135,6 +138,27 @@ uint64_t mix64(uint64_t z) {
   return z;
 }
 
+// Host loops over large scenes (config 5: 1M primitives, 400k nodes) in contiguous chunks on up to 16
+// threads (the GPU box's cgroup quota); fn(begin, end, t). Small ranges run inline.
+template <class F>
+void host_par_for(int64_t n, F&& fn) {
+  int T = static_cast<int>(std::thread::hardware_concurrency());
+  T = std::min(16, std::max(1, T));
+  if (n < 65536) T = 1;
+  if (T == 1) {
+    fn(int64_t(0), n, 0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back([&, t]() { fn(n * t / T, n * (t + 1) / T, t); });
+  fn(int64_t(0), n / T, 0);
+  for (auto& x : th) x.join();
+}
+int host_threads(int64_t n) {
+  const int T = std::min(16, std::max(1, static_cast<int>(std::thread::hardware_concurrency())));
+  return n < 65536 ? 1 : T;
+}
+
 bool texture_uses_uv(const rtg_scene_desc* d, int32_t tex, int depth) {
   if (depth > 16 || tex < 0 || tex >= d->num_textures) return false;
   const rtg_texture& t = d->textures[tex];
@@ -251,9 +275,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   auto tp = std::chrono::steady_clock::now();
   auto phase = [&](const char* what) {
     const auto now = std::chrono::steady_clock::now();
-    if (verbose)
-      std::fprintf(stderr, "[rtg] compile %-10s %8.1f ms\n", what,
-                   std::chrono::duration<double, std::milli>(now - tp).count());
+    const double ms = std::chrono::duration<double, std::milli>(now - tp).count();
+    if (verbose) std::fprintf(stderr, "[rtg] compile %-10s %8.1f ms\n", what, ms);
+    if (std::strcmp(what, "bvh") == 0) out->bvh_ms += ms;
+    if (std::strcmp(what, "collapse") == 0 || std::strcmp(what, "bfs") == 0) out->collapse_ms += ms;
     tp = now;
   };
   if (d->num_prims < 0 || (d->num_prims > 0 && !d->prims) || d->num_materials < 0 ||
@@ -299,15 +324,27 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   if ((d->bvh_mode == RTG_BVH_SAH || gpu_bvh) && d->num_prims > 1 && !std::getenv("RTG_NO_OCCLUDER")) {
     double slo[3] = {1e300, 1e300, 1e300}, shi[3] = {-1e300, -1e300, -1e300};
     std::vector<double> area(d->num_prims);
-    for (int64_t i = 0; i < d->num_prims; ++i) {
-      double lo[3], hi[3];
-      prim_bbox(d->prims[i], lo, hi);
-      for (int a = 0; a < 3; ++a) {
-        slo[a] = std::min(slo[a], lo[a]);
-        shi[a] = std::max(shi[a], hi[a]);
-      }
-      const double ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
-      area[i] = ex * ey + ey * ez + ez * ex;
+    {
+      const int T = host_threads(d->num_prims);
+      std::vector<std::array<double, 6>> part(T, {1e300, 1e300, 1e300, -1e300, -1e300, -1e300});
+      host_par_for(d->num_prims, [&](int64_t b, int64_t e, int t) {
+        std::array<double, 6>& m = part[t];
+        for (int64_t i = b; i < e; ++i) {
+          double lo[3], hi[3];
+          prim_bbox(d->prims[i], lo, hi);
+          for (int a = 0; a < 3; ++a) {
+            m[a] = std::min(m[a], lo[a]);
+            m[3 + a] = std::max(m[3 + a], hi[a]);
+          }
+          const double ex = hi[0] - lo[0], ey = hi[1] - lo[1], ez = hi[2] - lo[2];
+          area[i] = ex * ey + ey * ez + ez * ex;
+        }
+      });
+      for (const auto& m : part)
+        for (int a = 0; a < 3; ++a) {
+          slo[a] = std::min(slo[a], m[a]);
+          shi[a] = std::max(shi[a], m[3 + a]);
+        }
     }
     const double ex = shi[0] - slo[0], ey = shi[1] - slo[1], ez = shi[2] - slo[2];
     const double scene_area = ex * ey + ey * ez + ez * ex;
@@ -437,15 +474,6 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
 
   phase("prims");
   // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
-  auto leaf_code = [&](int32_t child, int32_t count, int32_t* code) {
-    const int64_t first = -(static_cast<int64_t>(child) + 1);
-    if (count < 1 || count > 8 || first >= (int64_t(1) << 28)) {
-      *err = "BVH leaf not encodable";
-      return false;
-    }
-    *code = ~static_cast<int32_t>((first << 3) | (count - 1));
-    return true;
-  };
   if (out->node_width == 4) {
     // 4-wide nodes, 112 B: lo.x[4], lo.y[4], lo.z[4], hi.x[4], hi.y[4], hi.z[4], code[4]
     if (bvh4.nodes.size() > static_cast<size_t>(INT32_MAX / 112)) {
@@ -453,27 +481,47 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       return false;
     }
     out->nodes.resize(bvh4.nodes.size() * 28);
-    for (size_t k = 0; k < bvh4.nodes.size(); ++k) {
-      const BuildNode4& n = bvh4.nodes[k];
-      float* f = &out->nodes[k * 28];
-      if (n.child[0] == kEmptyChild) {
+    const int64_t nn = static_cast<int64_t>(bvh4.nodes.size());
+    std::vector<int> bad(host_threads(nn), 0);  // 1: a node without children, 2: a leaf not encodable
+    host_par_for(nn, [&](int64_t b, int64_t e, int t) {
+      for (int64_t k = b; k < e && !bad[t]; ++k) {
+        const BuildNode4& n = bvh4.nodes[k];
+        float* f = &out->nodes[k * 28];
+        if (n.child[0] == kEmptyChild) {
+          bad[t] = 1;
+          break;
+        }
+        for (int c = 0; c < 4; ++c) {
+          int32_t code = kEmptyChild;
+          const bool empty = n.child[c] == kEmptyChild;
+          if (!empty) {
+            if (n.child[c] >= 0) {
+              code = n.child[c] * 112;  // inner children: byte offset of the node
+            } else {
+              const int64_t first = -(static_cast<int64_t>(n.child[c]) + 1);
+              if (n.count[c] < 1 || n.count[c] > 8 || first >= (int64_t(1) << 28)) {
+                bad[t] = 2;
+                break;
+              }
+              code = ~static_cast<int32_t>((first << 3) | (n.count[c] - 1));
+            }
+          }
+          for (int a = 0; a < 3; ++a) {
+            f[a * 4 + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
+            f[12 + a * 4 + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
+          }
+          f[24 + c] = ibits_to_float(code);
+        }
+      }
+    });
+    for (const int b : bad) {
+      if (b == 1) {
         *err = "4-wide BVH node without children";
         return false;
       }
-      for (int c = 0; c < 4; ++c) {
-        int32_t code = kEmptyChild;
-        const bool empty = n.child[c] == kEmptyChild;
-        if (!empty) {
-          if (n.child[c] >= 0)
-            code = n.child[c] * 112;  // inner children: byte offset of the node
-          else if (!leaf_code(n.child[c], n.count[c], &code))
-            return false;
-        }
-        for (int a = 0; a < 3; ++a) {
-          f[a * 4 + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
-          f[12 + a * 4 + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
-        }
-        f[24 + c] = ibits_to_float(code);
+      if (b == 2) {
+        *err = "BVH leaf not encodable";
+        return false;
       }
     }
   }
@@ -881,6 +929,9 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->info.device_bytes = static_cast<int64_t>(total);
   s->info.build_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() + gpu_build_ms;
   s->info.upload_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  s->info.bvh_ms = hs.bvh_ms + gpu_build_ms;
+  s->info.collapse_ms = hs.collapse_ms;
+  s->info.flatten_ms = std::chrono::duration<double, std::milli>(t1 - t0).count() - hs.bvh_ms - hs.collapse_ms;
   *out = s;
   return RTG_OK;
 }

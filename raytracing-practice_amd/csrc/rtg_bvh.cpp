@@ -796,6 +796,7 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
       return me;
     }
   } rec{bin, out, slot_of, prm.sah ? &dp : nullptr};
+  out->nodes.reserve(bin.nodes.size() / 2 + 2);
   out->nodes.push_back(BuildNode4{});  // the root is node 0
   rec.fill(0, 0, 1, 0);
 }

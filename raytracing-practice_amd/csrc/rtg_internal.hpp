@@ -45,6 +45,7 @@ struct HostScene {
   int64_t occluder_prim = -1;  // input primitive kept out of the BVH (a sphere; -1: none)
   int32_t occluder = -1;       // its sphere index (stored after the BVH-referenced spheres)
   int64_t node_capacity = 0;  // gpu_bvh: 4-wide nodes to reserve
+  double bvh_ms = 0.0, collapse_ms = 0.0;  // host build phases (rtg_scene_info)
 };
 
 // Double-precision BVH produced by the builders (child-pair form, pre-order DFS).

@@ -106,7 +106,8 @@ class rtg_render_stats(C.Structure):
 class rtg_scene_info(C.Structure):
     _fields_ = [("device", C.c_int32), ("bvh_mode", C.c_int32), ("num_prims", C.c_int64),
                 ("num_nodes", C.c_int64), ("bvh_depth", C.c_int32), ("stack_depth", C.c_int32),
-                ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("upload_ms", C.c_double)]
+                ("device_bytes", C.c_int64), ("build_ms", C.c_double), ("upload_ms", C.c_double),
+                ("bvh_ms", C.c_double), ("collapse_ms", C.c_double), ("flatten_ms", C.c_double)]
 
 
 class rtg_launch_plan(C.Structure):

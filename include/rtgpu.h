@@ -293,7 +293,9 @@ typedef struct rtg_launch_plan {
   int32_t chunks;
   int64_t partial_bytes;     /* device scratch of the chunk partial sums this render allocates */
   int32_t num_cus;
-  int32_t reserved_[7];
+  int32_t tile_slots;        /* > 0: chunks are summed per tile through a ring of this many tile
+                                slots (partial_bytes = ring + slot words); 0: full-frame partials */
+  int32_t reserved_[6];
 } rtg_launch_plan;
 
 rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,

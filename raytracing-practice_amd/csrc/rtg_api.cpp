@@ -29,7 +29,7 @@ hipError_t launch_render(const KernelChoice& k, const DevScene& S, const DevCame
 KernelResources kernel_resources(const void* fn);
 int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J);
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J);
-bool dual_fits_registers(bool count, bool verbose);
+bool dual_fits_registers(bool count, bool ring, bool verbose);
 hipError_t launch_resolve(const float* in, uint8_t* out, int64_t n_pixels, hipStream_t stream);
 }  // namespace rtg
 
@@ -50,7 +50,8 @@ constexpr int kSmallBvhNodes = 16;
 constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
-constexpr int kNumCounters = 24;        // [0..6] see DevJob::counters, [8..23] diagnostics
+constexpr int64_t kRingAutoBytes = int64_t(4) << 30;  // full-frame partials above this: the tile ring
+constexpr int kNumCounters = 26;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring)
 // gfx950 allocates a workgroup's LDS in 1280-byte granules (160 KB = 128 of them): measured with the
 // dual launch, whose two workgroups stop sharing a CU exactly when the rounded sizes pass 160 KB
 constexpr int kLdsGranule = 1280;
@@ -230,6 +231,8 @@ Knobs read_knobs() {
   num("RTG_DUAL", 0, 1, &k.dual);
   int st = 0;
   if (num("RTG_STACK", 16, 64, &st) && (st == 16 || st == 32 || st == 64)) k.stack = st;
+  int ts = 0;  // tile-ring slots: 0 or a power of two (tests shrink the ring to force slot waits)
+  if (num("RTG_TILE_SLOTS", 0, 65536, &ts) && (ts & (ts - 1)) == 0) k.tile_slots = ts;
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -985,6 +988,8 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   if (c[4] != 0)
     return fail(RTG_E_UNSUPPORTED, "BVH traversal stack overflow in " + std::to_string(c[4]) + " waves");
   if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
+  if (c[24] != 0)
+    return fail(RTG_E_HIP, "tile-ring slot waits timed out (frame incomplete) in " + std::to_string(c[24]) + " waves");
   if (c[7] != 0)
     return fail(RTG_E_UNSUPPORTED, "the 16-bit LDS stack layout cannot hold this tree's codes in " +
                                        std::to_string(c[7]) + " workgroups (nothing rendered)");
@@ -1009,6 +1014,8 @@ struct Plan {
   int lds_bytes = -1, lds4 = -1, lds_wgs = 1;
   int stack_depth = 0, grid_blocks = 1, grid_waves = 0;
   bool default_sched = false, chunked = false, skip_kernel = false;
+  int ring_slots = 0;  // chunked: tile slots of the partial-sum ring (0: full-frame partials + combine_kernel)
+  size_t ring_bytes = 0;
   int sum_chunks = 1;
   float out_scale = 1.0f;
   size_t out_bytes = 0;
@@ -1102,6 +1109,16 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     P->out_scale = P->sum_chunks == total_chunks ? dc.scale : 1.0f / static_cast<float>(samples_done);
   }
 
+  // one-shot chunked frames of the default schedules sum each tile's chunks through the tile ring
+  // (RING kernels; the counting kernels keep the full-frame partials, same frame)
+  // By default only where the full-frame partial buffers would be large (config 5's 6.3 GB): the ring
+  // costs the render loop time (config 5 +2.8 %, config 2 +7.5 %, config 4 +17 %: DESIGN.md §9), the
+  // full-frame buffers cost memory. RTG_TILE_SLOTS=0 / >0 forces it off / on.
+  const int64_t full_partial_bytes = int64_t(rows) * W * 12 * dj.chunks;
+  const bool ring_on = K.tile_slots > 0 || (K.tile_slots < 0 && full_partial_bytes > kRingAutoBytes);
+  const bool want_ring = !P->progressive && dj.chunks > 1 && dj.chunks <= (1 << 20) && dc.max_depth > 0 &&
+                         !P->count && ring_on;
+  dj.ring_log2 = want_ring ? 0 : -1;  // provisional: the LDS layouts reserve the per-wave batch tables
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
   // traversal stack: 16 LDS entries for the persistent kernel, 16 or 32 for the plain grid (the
@@ -1143,7 +1160,7 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   DevJob j4{};
   int lds4 = -1;
   if (dj.lds_waves == kLdsWaves && stk16 && !dscene.tex_full && K.dual != 0 && K.lds_waves != 16 &&
-      dual_fits_registers(P->count, K.verbose)) {
+      dual_fits_registers(P->count, want_ring, K.verbose)) {
     for (const int f4 : {3, 2}) {
       DevJob a = dj, b = dj;
       a.lds_sphere_f4 = b.lds_sphere_f4 = f4;
@@ -1202,6 +1219,26 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   if (P->progressive && !P->default_sched)
     return fail(RTG_E_INVALID, "progressive rendering needs the default schedules");
   P->chunked = !P->progressive && dj.chunks > 1 && P->default_sched && dc.max_depth > 0;
+  dj.ring_log2 = -1;
+  dj.ring_words = nullptr;
+  if (P->chunked && want_ring) {
+    // per-tile combine: R tile slots of chunks x 64 float4 partials. R * chunks is
+    // ~2^17 batches, about 8x the span between the oldest unfinished tile and the newest handed out
+    // (a slot that is still in use only delays a batch); a ring of at least the shard's tiles never waits
+    int lg = 0;
+    if (K.tile_slots > 0) {
+      while ((1 << lg) < K.tile_slots) ++lg;
+    } else {
+      while ((static_cast<int64_t>(2) << lg) * dj.chunks <= (int64_t(1) << 17)) ++lg;
+    }
+    while (lg > 0 && (1 << (lg - 1)) >= dj.num_tiles) --lg;  // no more slots than tiles
+    // a unit's ring index (< 2^28, packed beside its entry) and the ring's byte size (< 2^31, one
+    // buffer descriptor) bound the ring
+    while (lg > 0 && (static_cast<int64_t>(dj.chunks) << (lg + 10)) >= (int64_t(1) << 31)) --lg;
+    dj.ring_log2 = lg;
+    P->ring_slots = 1 << lg;
+    P->ring_bytes = (static_cast<size_t>(dj.chunks) << (lg + 10)) + (size_t(8) << lg);
+  }
   if (!P->default_sched) {  // schedules 1 and 2 keep one running sum per pixel
     dj.chunks = 1;
     dj.chunk_samples = std::max(1, cam->samples_per_pixel);
@@ -1210,12 +1247,13 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   if (P->skip_kernel || variant != 3) lds4 = -1;
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
-                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks};
+                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks, j4.lds_ring};
     j4 = dj;
     j4.lds_waves = 4;
     j4.lds_nodes = l4[0], j4.lds_refs = l4[1], j4.lds_spheres = l4[2], j4.lds_quads = l4[3];
     j4.lds_materials = l4[4], j4.lds_textures = l4[5], j4.lds_perlin_vec = l4[6], j4.lds_perlin_perm = l4[7];
     j4.lds_stacks = l4[8];
+    j4.lds_ring = l4[9];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
   P->j4 = j4;
@@ -1272,7 +1310,9 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
   out->leaf_batch = P.dj.leaf_batch;
   out->chunk_samples = P.dj.chunk_samples;
   out->chunks = P.dj.chunks;
-  out->partial_bytes = P.chunked ? static_cast<int64_t>(P.out_bytes) * P.dj.chunks : 0;
+  out->partial_bytes = !P.chunked ? 0 : P.ring_slots ? static_cast<int64_t>(P.ring_bytes)
+                                                     : static_cast<int64_t>(P.out_bytes) * P.dj.chunks;
+  out->tile_slots = P.ring_slots;
   out->num_cus = s->num_cus;
   return RTG_OK;
 }
@@ -1326,7 +1366,14 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
   }
-  if (P.chunked) {
+  if (P.chunked && P.ring_slots) {  // [slot words: gen R, ticket R][ring of tile slots]
+    RTG_HIP(hipMallocAsync(scratch.add(), P.ring_bytes, stream), "hipMallocAsync(tile ring)");
+    unsigned char* base = static_cast<unsigned char*>(scratch.ptr[scratch.n - 1]);
+    const size_t words = size_t(8) * P.ring_slots;  // a multiple of 16 B at the allocation's start
+    RTG_HIP(hipMemsetAsync(base, 0, words, stream), "hipMemsetAsync(tile ring words)");
+    dj.ring_words = reinterpret_cast<uint32_t*>(base);
+    dj.partial = reinterpret_cast<float*>(base + words);
+  } else if (P.chunked) {
     RTG_HIP(hipMallocAsync(scratch.add(), out_bytes * dj.chunks, stream), "hipMallocAsync(partial sums)");
     dj.partial = static_cast<float*>(scratch.ptr[scratch.n - 1]);
   }
@@ -1345,6 +1392,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     j4.counters = dj.counters;
     j4.spill = dj.spill;
     j4.partial = dj.partial;
+    j4.ring_words = dj.ring_words;
     // the aux launch must sit in a hardware queue of its own, or it only starts after the main launch
     // has drained (HIP shares its GPU_MAX_HW_QUEUES = 4 queues round-robin among a process's streams:
     // with RCCL or a second library's streams the two launches serialised, +10 %); high-priority
@@ -1366,7 +1414,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     RTG_HIP(hipEventRecord(s->ev_join, s->aux_stream), "hipEventRecord");
     RTG_HIP(hipStreamWaitEvent(stream, s->ev_join, 0), "hipStreamWaitEvent");
   }
-  if (P.chunked || (P.progressive && dout))
+  if ((P.chunked && !P.ring_slots) || (P.progressive && dout))
     RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, P.sum_chunks, P.out_scale, stream),
             "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");

@@ -209,7 +209,8 @@ struct Knobs {
   int lds_waves = 0;            // RTG_LDS_WAVES 4 | 16 (0: by scene size)
   int dual = -1;                // RTG_DUAL 0 | 1 (-1: where it fits)
   int stack = 0;                // RTG_STACK 16 | 32 | 64 (A/B schedules only)
-  std::string wave_trace;       // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
+  int tile_slots = -1;          // RTG_TILE_SLOTS 0 (full-frame partials) | 1..65536 (-1: by chunks)
+  std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
 };
 Knobs read_knobs();
 
@@ -222,7 +223,9 @@ struct DevJob {
   float* out;
   // [0] segments, [1] box tests, [2] prim tests, [3] hits, [4] stack overflow, [5] bad BVH code,
   // [6] persistent kernels' tile counter, [7] workgroups that could not run the 16-bit LDS stack
-  // layout (codes past 16 bits: RTG_E_UNSUPPORTED, nothing rendered), [8..23] schedule diagnostics
+  // layout (codes past 16 bits: RTG_E_UNSUPPORTED, nothing rendered), [8..23] schedule diagnostics,
+  // [24] tile-ring waits that timed out (RTG_E_INTERNAL: frame incomplete), [25] batches that found
+  // their ring slot still owned by an earlier tile (waits; diagnostic)
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 64-pixel tiles per shard row of tiles
@@ -230,9 +233,17 @@ struct DevJob {
   int32_t tile_lw;    // log2 tile width: 3 = 8x8 shard pixels, 4 = 16x4, 5 = 32x2 (row-strided shards)
   int32_t chunks;         // sample chunks rendered by this launch (work units = pixel x chunk)
   int32_t chunk_begin;    // first of them (progressive rendering; 0 for a one-shot frame)
-  int32_t pad4_;
+  // chunks > 1, one-shot frame: log2 of the tile slots of the partial-sum ring (the chunks of a
+  // tile are summed by the wave whose batch of that tile finishes last; DESIGN.md §4 "per-tile
+  // combine"); -1: progressive rendering or one chunk (partial, if any, is the full-frame layout)
+  int32_t ring_log2;
   int32_t chunk_samples;  // K: samples per chunk (the last chunk may be shorter)
-  float* partial;         // chunks > 1: [chunk][row][column][3] partial sums; else null
+  // ring_log2 >= 0: [slot][chunk][64 tile pixels] float4 partial sums (rgb, pad), written sc1;
+  // else chunks > 1: [chunk][row][column][3] partial sums; else null
+  float* partial;
+  // ring_log2 >= 0: [0, R) slot generation (the tile that may write slot s next is gen * R + s),
+  // [R, 2R) slot ticket (batches finished in the slot, all generations); zeroed before every launch
+  uint32_t* ring_words;
   int32_t* spill;         // traversal-stack entries beyond the LDS part: [wave][depth][lane]
   int32_t spill_depth;    // entries per lane in `spill` (0: the LDS stack suffices)
   int32_t lds_stack;      // stack entries kept in LDS (the kernel's STACK; tests may lower it)
@@ -246,6 +257,7 @@ struct DevJob {
   int32_t lds_waves;                         // persistent LDS kernel: waves per workgroup
   int32_t stack_esz;                         // persistent kernels: bytes per LDS stack entry (2 or 4)
   int32_t lds_stacks;                        // persistent kernels: byte offset of the traversal stacks in LDS
+  int32_t lds_ring;                          // RING kernels: byte offset of the per-wave batch tables (64 B each)
 
 };
 

@@ -1003,6 +1003,137 @@ __device__ __forceinline__ void start_pixel_sample(PathState& ps, const DevCamer
   start_sample(ps, C, J.seed_mix, pixel_id, sample, i, j);
 }
 
+// ---- per-tile combine through a ring of tile slots (DESIGN.md §4 "per-tile combine") ----
+// A one-shot chunked frame keeps no full-frame partial buffers: tile t owns ring slot t mod R,
+// [chunk][64 pixels] float4 partial sums. The wave that takes batch (t, c) writes its 64 partials
+// there with write-through (sc1) stores; when the batch's last unit has finished, the wave drains its
+// stores (s_waitcnt vmcnt(0)) and adds 1 to the slot's ticket (relaxed, agent scope). The wave whose
+// add is the tile's last (ticket = (gen + 1) * chunks - 1, tickets count every generation of the
+// slot) takes an agent-scope acquire, sums the tile's partials in chunk order
+// (((p0 + p1) + p2) + ..., the order combine_kernel uses), writes the 64 pixels and hands the slot to
+// tile t + R by storing gen + 1. A batch whose slot still belongs to tile t - R is pending: its wave
+// keeps running the units it holds and hands none of the batch out until the slot is free; a wave that
+// holds nothing but a pending batch sleeps on the slot word (bounded: counters[24] on timeout). Every
+// batch of tile t - R was handed out before any of tile t (tile-major hand-out), and a wave that
+// holds units never sleeps, so the oldest unfinished tile always progresses.
+// The hand-off is the split-K fan-in form of cdna_hip_programming.md Guideline 16: every storing wave
+// stores sc1 and drains before its counter add; the last adder, told by its add's return value, takes
+// ONE agent acquire before its plain loads; the slot word is an agent-scope atomic store after the
+// loader's own drain.
+// batches one wave tracks at once (a batch lives in one wave): a 64-B table per wave in LDS (entry:
+// tile << 7 | units of the batch not yet finished), so the count costs the render loop no SGPRs
+// (kept in SGPRs, 4 entries cost config 2 +16 % and config 4 +34 %, 8 entries more: profiles/r03_i)
+constexpr int kRingEntries = 16;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef unsigned int ring_u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bool ring_slot_free(const DevJob& J, int tile) {
+  const int slot = tile & ((1 << J.ring_log2) - 1);
+  const uint32_t g = __hip_atomic_load((gu32*)(J.ring_words + slot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(g)) == static_cast<uint32_t>(tile >> J.ring_log2);
+}
+
+// A unit's partial sum: 16 B per lane, one write-through store (aux 16 = sc1).
+__device__ __forceinline__ void ring_store(__amdgpu_buffer_rsrc_t rs, uint32_t unit, V3 a) {
+  const ring_u4 v = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), 0u};
+#if defined(RTG_AB_RING_PLAINSTORE) || defined(RTG_RING_RELEASE)
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>(unit << 4), 0, 0);
+#else
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>(unit << 4), 0, 16);
+#endif
+}
+
+// The tile's combine, by the wave whose ticket add was the tile's last: ONE agent acquire, the
+// partials in chunk order, the 64 pixels, then the slot to tile + R. It runs at the top of the render
+// loop, where every lane's path and traversal state is live and the 96-register dual-launch build has
+// no register to spare: one colour channel at a time through the ring's buffer descriptor keeps its
+// temporaries to a few registers (a float4 accumulator + float4 loads spilled the traversal state
+// across the trip loop: config 2 +14 %, config 4 +26 %, profiles/r03_m).
+template <bool WIDE_REGS>
+__device__ __forceinline__ void ring_combine(__amdgpu_buffer_rsrc_t rs, const DevCamera& C, const DevJob& J,
+                                             int tile, int slot) {
+  const int lane = __lane_id();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int ty = tile / J.tiles_x;
+  const int i = ((tile - ty * J.tiles_x) << J.tile_lw) + (lane & ((1 << J.tile_lw) - 1));
+  const int lr = (ty << (6 - J.tile_lw)) + (lane >> J.tile_lw);
+  // the pixel's byte offset in the frame (past the frame's end for pixels outside the image: the
+  // buffer descriptor's range check drops those stores)
+  const int frame_bytes = J.row_count * C.width * 12;
+  const int pix = i < C.width && lr < J.row_count ? (lr * C.width + i) * 12 : frame_bytes;
+  const __amdgpu_buffer_rsrc_t fs = __builtin_amdgcn_make_buffer_rsrc(J.out, 0, frame_bytes, 0x00020000);
+  const int base = (slot * J.chunks * 64 + lane) << 4;  // byte offset of this lane's chunk-0 partial
+  if constexpr (WIDE_REGS) {
+    // registers to spare (the 128-VGPR treelet build): whole partials, eight loads in flight, the
+    // adds still in chunk order
+    const ring_u4 p0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
+    float ax = __uint_as_float(p0.x), ay = __uint_as_float(p0.y), az = __uint_as_float(p0.z);
+    int c = 1;
+    for (; c + 8 <= J.chunks; c += 8) {
+      ring_u4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, base + ((c + k) << 10), 0, 0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ax = ax + __uint_as_float(v[k].x);
+        ay = ay + __uint_as_float(v[k].y);
+        az = az + __uint_as_float(v[k].z);
+      }
+    }
+    for (; c < J.chunks; ++c) {
+      const ring_u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, base + (c << 10), 0, 0);
+      ax = ax + __uint_as_float(v.x);
+      ay = ay + __uint_as_float(v.y);
+      az = az + __uint_as_float(v.z);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(C.scale * ax), fs, pix, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(C.scale * ay), fs, pix, 4, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(C.scale * az), fs, pix, 8, 0);
+  } else {
+    // the 96-VGPR builds: one colour channel at a time, one load in flight
+    for (int ch = 0; ch < 3; ++ch) {
+      float a = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base, ch * 4, 0));
+#pragma unroll 1
+      for (int c = 1; c < J.chunks; ++c)
+        a = a + __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, base + (c << 10), ch * 4, 0));
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(C.scale * a), fs, pix, ch * 4, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot's loads returned: hand it on
+  if (lane == 0)
+    __hip_atomic_store((gu32*)(J.ring_words + slot), static_cast<uint32_t>(tile >> J.ring_log2) + 1u,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Batch (tile, any chunk) finished in this wave: drain, ticket add, and the tile's combine if this
+// add was the tile's last. Wave-uniform call (all 64 lanes active).
+template <bool WIDE_REGS>
+__device__ __forceinline__ void ring_batch_done(__amdgpu_buffer_rsrc_t rs, const DevCamera& C, const DevJob& J,
+                                                int tile) {
+#ifdef RTG_RING_RELEASE  // plain partial stores: drain, agent release (L2 write-back), drain again
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#elif !defined(RTG_AB_RING_NOWAIT)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have landed
+#endif
+  const int R = 1 << J.ring_log2;
+  const int slot = tile & (R - 1);
+  const uint32_t gen = static_cast<uint32_t>(tile >> J.ring_log2);
+  uint32_t old = 0;
+  if (__lane_id() == 0)
+    old = __hip_atomic_fetch_add((gu32*)(J.ring_words + R + slot), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __builtin_amdgcn_readfirstlane(old);
+  if (old + 1u != (gen + 1u) * static_cast<uint32_t>(J.chunks)) return;
+#ifdef RTG_AB_RING_NOCOMBINE
+  if (__lane_id() == 0)
+    __hip_atomic_store((gu32*)(J.ring_words + slot), gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return;
+#endif
+  ring_combine<WIDE_REGS>(rs, C, J, tile, slot);
+}
+
 // One wave renders a stream of work units with the ballot-batched schedule. A unit is one pixel
 // and one chunk of its samples: samples [c*K, min((c+1)*K, spp)) of chunk c (DESIGN.md §4 "sample
 // chunks"); a lane walks the chunk's samples in order, accumulating them from zero, and stores the
@@ -1017,9 +1148,9 @@ __device__ __forceinline__ void start_pixel_sample(PathState& ps, const DevCamer
 // or a leaf step for the whole wave (leaf work waits until leaf_batch lanes have reached a leaf);
 // the wave switches to shading once ceil(alive * shade_batch / 64) lanes have finished their
 // closest-hit query, and lanes still traversing keep their stack and continue afterwards.
-template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM>
+template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM, bool RING>
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                              const Stk& stk, WaveStats<COUNT>& w) {
+                                              const Stk& stk, WaveStats<COUNT>& w, lu32* rtab) {
   const int lane = __lane_id();
   const bool no_work = C.max_depth <= 0 || C.spp <= 0;  // every pixel is black (camera.hpp:192)
   const int num_batches = J.num_tiles * J.chunks;
@@ -1036,6 +1167,21 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   // wave-uniform: the current batch's tile origin and chunk, and its next unassigned unit
   int bx = 0, by = 0, bc = 0, k_next = 64;
   bool exhausted = false;
+  // tile ring (J.ring_log2 >= 0): the entries of rtab in use (the batches this wave holds), the
+  // entry of the batch being handed out, whether that batch waits for its slot; a lane's `chunk`
+  // then holds its unit's ring index | entry << 28, and `fin` marks a unit finished since the last
+  // settle
+  constexpr bool ring = RING;  // the host sets J.ring_log2 >= 0 exactly for the RING kernels
+  uint32_t e_used = 0;
+  int cur_e = 0;
+  bool pending = false, fin = false, exhausted_by_timeout = false;
+  uint32_t pend_spins = 0;  // empty trips spent waiting for the pending batch's slot
+  // the tile of the batch being handed out (from its origin: no state of its own)
+  auto cur_tile = [&]() { return (by >> (6 - J.tile_lw)) * J.tiles_x + (bx >> J.tile_lw); };
+  __amdgpu_buffer_rsrc_t ring_rs = __builtin_amdgcn_make_buffer_rsrc(J.partial, 0, 0, 0x00020000);
+  if (ring)
+    ring_rs = __builtin_amdgcn_make_buffer_rsrc(
+        J.partial, 0, static_cast<int>((static_cast<uint32_t>(J.chunks) << (J.ring_log2 + 10))), 0x00020000);
   PathState ps = {};
   Trav tr = {};
   tr.todo = kTravDone;
@@ -1043,10 +1189,41 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   for (;;) {
     uint64_t t_top = 0;
     if (COUNT) t_top = __builtin_amdgcn_s_memtime();
+    if (ring) {  // settle: count the units finished since the last trip, finish completed batches
+      uint64_t fm = ballot(fin);
+      if (fm != 0) {
+        const int ent = static_cast<int>(static_cast<uint32_t>(chunk) >> 28);
+        do {  // one LDS update per entry among the finished units (usually one)
+          const int e = __builtin_amdgcn_readlane(ent, static_cast<int>(__builtin_ctzll(fm)));
+          const uint64_t m = ballot(fin && ent == e);
+          const uint32_t n = static_cast<uint32_t>(__popcll(m));
+          uint32_t left = 0;
+          if (lane == 0) left = __hip_atomic_fetch_sub(rtab + e, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) - n;
+          left = __builtin_amdgcn_readfirstlane(left);
+          if ((left & 127u) == 0) {  // the batch's last unit: ticket (and the tile's combine)
+            e_used &= ~(1u << e);
+            ring_batch_done<false>(ring_rs, C, J, static_cast<int>(left >> 7));
+          }
+          fm &= ~m;
+        } while (fm != 0);
+        fin = false;
+      }
+      if (pending) {  // the held batch waits for its slot: one poll per trip (empty trips sleep)
+        pending = !ring_slot_free(J, cur_tile());
+        if (pending && ballot(has()) == 0) {  // an empty trip: sleep, bounded (~2^22 trips, seconds)
+          __builtin_amdgcn_s_sleep(8);
+          if (++pend_spins > (1u << 22)) {
+            exhausted = exhausted_by_timeout = true;  // counters[24] after the loop; the wave drains
+            pending = false;
+          }
+        }
+      }
+    }
     // hand the next units of the current batch (new batches as needed) to the lanes without one
     uint64_t want = ballot(!has());
-    while (want != 0 && !exhausted) {
+    while (want != 0 && !exhausted && !pending) {
       if (k_next >= 64) {
+        if (ring && e_used == (1u << kRingEntries) - 1u) break;  // every entry busy: lanes wait
         int b = 0;
         if (lane == 0) b = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
         b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
@@ -1060,10 +1237,22 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         bx = (tile - ty * J.tiles_x) << J.tile_lw;
         by = ty << (6 - J.tile_lw);
         k_next = 0;
+        if (ring) {
+          cur_e = __builtin_ctz(~e_used);
+          e_used |= 1u << cur_e;
+          if (lane == 0) rtab[cur_e] = (static_cast<uint32_t>(tile) << 7) | 64u;
+          if (!ring_slot_free(J, tile)) {  // hand it out once its slot is free (top of the loop)
+            if (COUNT && lane == 0) atomicAdd(&J.counters[25], 1ull);
+            pending = true;
+            pend_spins = 0;
+            break;
+          }
+        }
       }
       const int take = min(__popcll(want), 64 - k_next);
       const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
           static_cast<uint32_t>(want >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(want), 0u)));
+      bool outside = false;  // a unit of the batch past the image edge: finished on hand-out
       if (!has() && rank < take) {
         const int k = k_next + rank;
         const int i = bx + (k & ((1 << J.tile_lw) - 1));
@@ -1077,12 +1266,21 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
             }
           } else {
             fresh = true;
-            chunk = bc;
+            chunk = ring ? ((((cur_tile() & ((1 << J.ring_log2) - 1)) * J.chunks + (bc - J.chunk_begin)) << 6) + k) |
+                               (cur_e << 28)
+                         : bc;
             sample = bc * J.chunk_samples;
             s_end = min(sample + J.chunk_samples, C.spp);
             acc = v3(0.0f, 0.0f, 0.0f);
           }
+        } else {
+          outside = true;
         }
+      }
+      if (ring) {
+        // units past the image edge finish on hand-out (a batch keeps >= 1 unit: its tile's origin)
+        const uint32_t n_out = static_cast<uint32_t>(__popcll(ballot(outside)));
+        if (n_out != 0 && lane == 0) rtab[cur_e] -= n_out;
       }
       k_next += take;
       want = ballot(!has());
@@ -1115,7 +1313,10 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     if (COUNT) w.diag[15] += __builtin_amdgcn_s_memtime() - t_start;  // trav_begin + occluder test
     const uint64_t has_m = ballot(has());  // constant over the trip loop: kept as an SGPR mask
     const int alive = __popcll(has_m);
-    if (alive == 0) break;
+    // the loop's one exit: nothing left to hand out and no unit in a lane. A wave whose only batch
+    // waits for its slot runs an empty trip and sleeps on the slot at the top of the loop (a second
+    // back edge here instead made the register allocator spill the traversal state: config 2 +14 %)
+    if (alive == 0 && !pending) break;
     const int need = (alive * J.shade_batch + 63) >> 6;
     uint64_t t_trav0 = 0;
     if (COUNT) t_trav0 = __builtin_amdgcn_s_memtime();
@@ -1197,16 +1398,29 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           fresh = true;
         } else {
           const int64_t pix = static_cast<int64_t>(px_lr(px)) * C.width + px_i(px);
-          if (J.partial == nullptr) {  // one chunk per pixel: the pixel mean directly
+          if (ring) {  // the unit's partial sum into its tile's ring slot (settled next trip)
+#ifdef RTG_AB_RING_NOSTORE
+            asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(chunk));  // probe: keep the values, skip the store
+#else
+            ring_store(ring_rs, static_cast<uint32_t>(chunk & 0x0fffffff), acc);
+#endif
+            fin = true;
+          } else if (J.partial == nullptr) {  // one chunk per pixel: the pixel mean directly
             float* o = J.out + pix * 3;
             o[0] = C.scale * acc.x;
             o[1] = C.scale * acc.y;
             o[2] = C.scale * acc.z;
-          } else {  // chunk partial sum, combined in chunk order by combine_kernel
+          } else {  // progressive: chunk partial sum in the full-frame layout, combined by combine_kernel
             float* o = J.partial + (static_cast<int64_t>(chunk) * J.row_count * C.width + pix) * 3;
+#ifdef RTG_AB_BASE_SC1  // probe: the full-frame partials stored write-through
+            __hip_atomic_store((gu32*)o, __float_as_uint(acc.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gu32*)(o + 1), __float_as_uint(acc.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store((gu32*)(o + 2), __float_as_uint(acc.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
             o[0] = acc.x;
             o[1] = acc.y;
             o[2] = acc.z;
+#endif
           }
           s_end = 0;  // the unit is done
           ++w.pixels;
@@ -1216,25 +1430,29 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     }
     if (COUNT) w.diag[6] += __builtin_amdgcn_s_memtime() - t_shade0;
   }
+  // a slot wait that timed out, or (unreachable) a held batch never combined: the frame is incomplete
+  if (ring && (exhausted_by_timeout || e_used != 0) && lane == 0) atomicAdd(&J.counters[24], 1ull);
 }
 
 // Schedule 4: the same loop on a plain grid of 256-thread workgroups (scene read through the
 // caches; used when it does not fit in LDS). Waves take tiles from the same counter.
-template <int STACK, bool SPILL, bool COUNT, int WIDE, bool TEXF>
+template <int STACK, bool SPILL, bool COUNT, int WIDE, bool TEXF, bool RING>
 __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, DevJob J) {
   __shared__ int32_t s_stack[4 * STACK * 64];
+  __shared__ uint32_t s_ring[RING ? 4 * kRingEntries : 1];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int slot = blockIdx.x * 4 + wave;
+  lu32* rtab = (lu32*)(s_ring) + (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
   int32_t* lstk = s_stack + wave * STACK * 64 + lane;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   WaveStats<COUNT> w;
   if constexpr (SPILL) {
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal>(S, C, J, stk, w);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, stk, w, rtab);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal>(S, C, J, LdsStack<STACK>{lstk}, w);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, LdsStack<STACK>{lstk}, w, rtab);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, slot, (blockIdx.x << 8) | wave);
@@ -1250,7 +1468,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 // persistent workgroups keep only the breadth-first top of the 4-wide tree in LDS (as many nodes as
 // fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
 // through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM>
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING>
 // WAVES = 4: compiled for 5 waves per SIMD (<= 96 VGPRs) and launched with 4-wave workgroups (small
 // scenes, the dual launch's second workgroup) or 16-wave ones (book-1's main launch): one binary for
 // both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
@@ -1269,6 +1487,8 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
   const int wave = threadIdx.x >> 6;
   int32_t* lstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
   int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
+  lu32* rtab = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_ring)) +
+               (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
   if constexpr (GEOM == kGeomTreelet) {
     float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
     for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += kFill) l_top[k] = S.nodes[k];
@@ -1282,9 +1502,9 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
       const int slot = blockIdx.x * wpb + wave;
       const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                   J.lds_stack, J.lds_stack + J.spill_depth};
-      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet>(L, C, J, stk, w);
+      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, stk, w, rtab);
     } else {
-      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet>(L, C, J, LdsStack<STACK>{lstk}, w);
+      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
     }
     flush_stats<COUNT>(J, w, lane);
     trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
@@ -1355,11 +1575,11 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
     const int slot = blockIdx.x * wpb + wave;
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, stk, w);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, stk, w, rtab);
   } else if constexpr (STK16) {
-    render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, LdsStack16<STACK>{lstk16}, w);
+    render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, LdsStack16<STACK>{lstk16}, w, rtab);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds>(L, C, J, LdsStack<STACK>{lstk}, w);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
@@ -1506,20 +1726,22 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int WAVES = kLdsWaves>
-KernelChoice lds_kernel(bool count, int threads = WAVES * 64) {
+KernelChoice lds_kernel(bool count, bool ring, int threads = WAVES * 64) {
   KernelChoice k;
-  k.fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM>)
-               : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM>);
+  k.fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM, false>)
+         : ring ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, true>)
+                : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, false>);
   k.block = threads;
   k.dynamic_lds = true;
   return k;
 }
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF>
-KernelChoice plain_kernel(bool count) {
+KernelChoice plain_kernel(bool count, bool ring) {
   KernelChoice k;
-  k.fn = count ? reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, true, WIDE, TEXF>)
-               : reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, false, WIDE, TEXF>);
+  k.fn = count ? reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, true, WIDE, TEXF, false>)
+         : ring ? reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, false, WIDE, TEXF, true>)
+                : reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, false, WIDE, TEXF, false>);
   k.block = 256;
   return k;
 }
@@ -1541,12 +1763,12 @@ KernelChoice legacy_kernel(bool count, int variant) {
 // Schedule 5: the persistent kernel with an LDS treelet over a scene in HBM (4-wide trees only).
 KernelChoice treelet_kernel(const DevScene& S, const DevJob& J, bool count) {
   if (S.node_width != 4 || J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves) return {};
-  const bool spill = J.spill_depth > 0, tex = S.tex_full != 0;
+  const bool spill = J.spill_depth > 0, tex = S.tex_full != 0, ring = J.ring_log2 >= 0 && !count;
   if (spill)
-    return tex ? lds_kernel<kLdsStack, true, 4, true, kGeomTreelet>(count)
-               : lds_kernel<kLdsStack, true, 4, false, kGeomTreelet>(count);
-  return tex ? lds_kernel<kLdsStack, false, 4, true, kGeomTreelet>(count)
-             : lds_kernel<kLdsStack, false, 4, false, kGeomTreelet>(count);
+    return tex ? lds_kernel<kLdsStack, true, 4, true, kGeomTreelet>(count, ring)
+               : lds_kernel<kLdsStack, true, 4, false, kGeomTreelet>(count, ring);
+  return tex ? lds_kernel<kLdsStack, false, 4, true, kGeomTreelet>(count, ring)
+             : lds_kernel<kLdsStack, false, 4, false, kGeomTreelet>(count, ring);
 }
 
 // The default schedules: persistent LDS kernel (16 LDS stack entries) or the plain grid (16, or 32
@@ -1555,6 +1777,7 @@ template <int WIDE>
 KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int stack, bool lds) {
   const bool spill = J.spill_depth > 0;
   const bool tex = S.tex_full != 0;
+  const bool ring = J.ring_log2 >= 0 && !count;
   if (lds) {
     if (stack != kLdsStack || J.lds_stack > kLdsStack) return {};
     // 4-wide trees keep 16-bit stack entries (J.stack_esz 2) unless their leaf codes do not fit 16
@@ -1563,21 +1786,21 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
     const bool stk16 = WIDE == 4 && !spill && !tex && J.stack_esz == 2;
     if (J.stack_esz != (stk16 ? 2 : 4)) return {};
     if (spill || (WIDE == 4 && !tex && !stk16))
-      return tex ? lds_kernel<kLdsStack, true, WIDE, true>(count) : lds_kernel<kLdsStack, true, WIDE, false>(count);
+      return tex ? lds_kernel<kLdsStack, true, WIDE, true>(count, ring) : lds_kernel<kLdsStack, true, WIDE, false>(count, ring);
     // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
     if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
-      return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, kLdsWaves * 64);
+      return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring, kLdsWaves * 64);
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU; the dual's second launch
-      return tex ? lds_kernel<kLdsStack, false, WIDE, true, kGeomLds, 4>(count)
-                 : lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count);
-    return tex ? lds_kernel<kLdsStack, false, WIDE, true>(count) : lds_kernel<kLdsStack, false, WIDE, false>(count);
+      return tex ? lds_kernel<kLdsStack, false, WIDE, true, kGeomLds, 4>(count, ring)
+                 : lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring);
+    return tex ? lds_kernel<kLdsStack, false, WIDE, true>(count, ring) : lds_kernel<kLdsStack, false, WIDE, false>(count, ring);
   }
   if (stack > 32 || J.lds_stack > stack) return {};
   if (spill)  // (any LDS part <= 32 entries, J.lds_stack, plus the global spill)
-    return tex ? plain_kernel<32, true, WIDE, true>(count) : plain_kernel<32, true, WIDE, false>(count);
+    return tex ? plain_kernel<32, true, WIDE, true>(count, ring) : plain_kernel<32, true, WIDE, false>(count, ring);
   if (stack == 16)
-    return tex ? plain_kernel<16, false, WIDE, true>(count) : plain_kernel<16, false, WIDE, false>(count);
-  return tex ? plain_kernel<32, false, WIDE, true>(count) : plain_kernel<32, false, WIDE, false>(count);
+    return tex ? plain_kernel<16, false, WIDE, true>(count, ring) : plain_kernel<16, false, WIDE, false>(count, ring);
+  return tex ? plain_kernel<32, false, WIDE, true>(count, ring) : plain_kernel<32, false, WIDE, false>(count, ring);
 }
 
 }  // namespace
@@ -1662,6 +1885,8 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   off = a16(off + int64_t(S.num_perlins) * 256 * 16);
   const int64_t pperm = off;
   off = a16(off + int64_t(S.num_perlins) * 768 * 4);
+  const int64_t ring = off;  // RING kernels (J->ring_log2 >= 0): per-wave batch tables
+  if (J && J->ring_log2 >= 0) off += int64_t(waves) * kRingEntries * 4;
   if (off > 160 * 1024) return -1;
   if (J) {
     J->lds_materials = static_cast<int32_t>(materials);
@@ -1673,6 +1898,7 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
     J->lds_refs = static_cast<int32_t>(refs);
     J->lds_perlin_vec = static_cast<int32_t>(pvec);
     J->lds_perlin_perm = static_cast<int32_t>(pperm);
+    J->lds_ring = static_cast<int32_t>(ring);
   }
   return static_cast<int>(off);
 }
@@ -1681,24 +1907,27 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
 // nodes as fit in the rest of one CU's 160 KiB; sets S.treelet_bytes and J.lds_nodes.
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
   const int64_t stacks = int64_t(waves) * stack * 64 * 4;
-  const int64_t room = 160 * 1024 - stacks;
+  const int64_t ring = J->ring_log2 >= 0 ? int64_t(waves) * kRingEntries * 4 : 0;  // RING: batch tables
+  const int64_t room = 160 * 1024 - stacks - ring;
   if (S->node_width != 4 || room < 112) return -1;
   const int64_t nodes = std::min<int64_t>(S->num_nodes, room / 112);
   S->treelet_bytes = static_cast<int32_t>(nodes * 112);
-  J->lds_nodes = static_cast<int32_t>(stacks);
+  J->lds_ring = static_cast<int32_t>(stacks);
+  J->lds_nodes = static_cast<int32_t>(stacks + ring);
   J->lds_stacks = 0;
-  return static_cast<int>(stacks + nodes * 112);
+  return static_cast<int>(stacks + ring + nodes * 112);
 }
 
 // The dual launch (rtg_api.cpp) needs the 16-wave workgroup's four waves and the 4-wave workgroup's
 // one wave of a SIMD to fit its 512 registers per lane together (allocation granule 8): checked on the
 // compiled kernel, so a later change that grows it drops the dual launch instead of leaving its
 // second workgroup to run after the first has taken all the work.
-bool dual_fits_registers(bool count, bool verbose) {
+bool dual_fits_registers(bool count, bool ring, bool verbose) {
   // both workgroups run the 4-wave build (default_kernel)
   const KernelResources r = kernel_resources(
-      count ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds>)
-            : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds>));
+      count  ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds, false>)
+      : ring ? reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds, true>)
+             : reinterpret_cast<const void*>(&render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds, false>));
   if (verbose) std::fprintf(stderr, "[rtg] dual check: numRegs %d\n", r.vgprs);
   if (!r.ok) return false;
   return 5 * ((r.vgprs + 7) / 8 * 8) <= 512;

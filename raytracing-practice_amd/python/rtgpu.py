@@ -115,7 +115,8 @@ class rtg_launch_plan(C.Structure):
         "schedule", "workgroups", "waves_per_workgroup", "lds_bytes", "vgprs", "sgprs", "scratch_bytes",
         "waves_per_simd", "dual", "dual_workgroups", "dual_lds_bytes", "dual_vgprs", "stack_entry_bytes",
         "lds_stack_entries", "spill_entries", "treelet_nodes", "shade_batch", "leaf_batch", "chunk_samples",
-        "chunks")] + [("partial_bytes", C.c_int64), ("num_cus", C.c_int32), ("reserved_", C.c_int32 * 7)]
+        "chunks")] + [("partial_bytes", C.c_int64), ("num_cus", C.c_int32), ("tile_slots", C.c_int32),
+                      ("reserved_", C.c_int32 * 6)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved_"}
@@ -164,6 +165,20 @@ def num_chunks(spp: int) -> int:
     return (spp + k - 1) // k if spp > 0 else 1
 
 
+def _one_hip_runtime():
+    """Load torch (when installed) before librtgpu.so, so the process holds ONE HIP runtime.
+
+    torch's wheel bundles its own libamdhip64; librtgpu.so links the system one under the same
+    soname. Loaded first, torch's copy also serves librtgpu.so and device pointers, streams and
+    events pass between the two freely. Loaded the other way round, the system runtime initialises the
+    device first and torch's later initialisation fails ("No HIP GPUs are available", MI355X box,
+    torch 2.10+rocm7.0 beside ROCm 7.2)."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 class Library:
     """librtgpu.so. Loading it requires the built library (make -C raytracing-practice_amd)."""
 
@@ -172,6 +187,7 @@ class Library:
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} not built (run __graft_entry__.build())")
         self.path = path
+        _one_hip_runtime()
         L = self.lib = C.CDLL(path)
         L.rtg_abi_version.restype = C.c_uint32
         L.rtg_last_error.restype = C.c_char_p
@@ -457,6 +473,7 @@ class SceneLibrary:
         path = path or os.path.join(LIB_DIR, "librtscenes.so")
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} not built (run __graft_entry__.build())")
+        _one_hip_runtime()
         L = self.lib = C.CDLL(path)
         L.rts_build.argtypes = [C.c_char_p, _P(rts_params), _P(C.c_void_p)]
         L.rts_build.restype = C.c_int32

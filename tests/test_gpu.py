@@ -312,6 +312,56 @@ def test_sample_chunks_match_oracle(gpu_lib, scenes, oracle, spp):
     assert np.array_equal(g, gs)  # deterministic whatever order the units ran in
 
 
+@pytest.mark.parametrize("name,W,spp,schedule", [
+    ("bouncing_spheres", 240, 40, 3), ("cornell_box", 96, 64, 3), ("bouncing_spheres", 160, 40, 5)])
+def test_tile_ring_matches_full_frame_partials(gpu_lib, scenes, name, W, spp, schedule, monkeypatch):
+    """One-shot chunked frames can sum each tile's chunks in chunk order in the wave whose batch of the
+    tile finished last, through a ring of tile slots (DESIGN.md §4 "per-tile combine"; the default
+    above 4 GiB of full-frame partials). The frame and the segment count must be those of the
+    full-frame partial buffers + combine kernel (RTG_TILE_SLOTS=0) for a ring with a slot per tile
+    and for rings of 1, 2 and 8 slots, where nearly every batch finds its slot still owned by an
+    earlier tile and waits (book-1: the dual launch; Cornell: 4-wave workgroups; schedule 5: the
+    treelet kernel)."""
+    import ctypes as C
+
+    s = scenes.build(name, rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = W, spp, 50
+    assert rtgpu.num_chunks(spp) >= 3
+    H = gpu_lib.camera_resolve(c).image_height
+    out = {}
+    for slots in ("0", "1", "2", "8", "65536", None):
+        if slots is None:
+            monkeypatch.delenv("RTG_TILE_SLOTS", raising=False)
+        else:
+            monkeypatch.setenv("RTG_TILE_SLOTS", slots)
+        ds = gpu_lib.scene_create(s.desc)
+        p = ds.plan(c)
+        assert p.chunks >= 3
+        if p.tile_slots:  # the ring and its slot words
+            assert p.partial_bytes == p.tile_slots * (p.chunks * 1024 + 8)
+        else:  # full-frame [chunk][row][column][3] partials
+            assert p.partial_bytes == H * W * 12 * p.chunks
+        if slots == "65536":  # more slots than tiles: one slot per tile (the ring never waits)
+            tiles = -(-W // 8) * -(-H // 8)
+            assert tiles <= p.tile_slots < 2 * tiles
+        elif slots is None:  # small frames keep the full-frame partials by default
+            assert p.tile_slots == 0
+        else:
+            assert p.tile_slots == int(slots)
+        frame = np.zeros((H, W, 3), dtype=np.float32)
+        st = rtgpu.rtg_render_stats()
+        job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, 0, 1, 0, rtgpu.RTG_RENDER_SCHEDULE(schedule), None)
+        gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job),
+                                                            frame.ctypes.data, C.byref(st)))
+        ds.close()
+        out[slots] = (frame, st.segments)
+    ref, ref_segs = out.pop("0")
+    assert float(ref.sum()) > 0.0
+    for slots, (frame, segs) in out.items():
+        assert np.array_equal(frame, ref) and segs == ref_segs, slots
+
+
 def test_progressive_chunks_and_checkpoint(gpu_lib, scenes):
     """Progressive rendering (rtg_render_desc.partial): chunks rendered in several calls, with a
     checkpoint (partial sums copied to the host, the scene destroyed and rebuilt) in between,
@@ -786,6 +836,16 @@ def test_render_plan_names_the_kernel(gpu_lib, scenes, name, grid, W, schedule, 
     assert (p.schedule, p.dual, p.waves_per_simd) == (schedule, dual, waves_per_simd), p.as_dict()
     assert 0 < p.vgprs <= 512 // waves_per_simd and p.chunks == 32 and p.chunk_samples == 16
     assert p.num_cus > 0 and p.workgroups > 0
+    H = gpu_lib.camera_resolve(c).image_height
+    assert p.tile_slots == 0 and p.partial_bytes == H * W * 12 * 32, p.as_dict()  # < 4 GiB: full-frame
+    if grid == 500:  # config 5 as benchmarked (1000 spp): 6.3 GB of full-frame partials -> the tile
+        # ring, ~2^17 batches of 1 KiB (R * chunks) plus 8 B of slot words per slot
+        c.samples_per_pixel = 1000
+        ds = gpu_lib.scene_create(s.desc)
+        p = ds.plan(c)
+        ds.close()
+        assert p.chunks == 63 and p.tile_slots == 2048, p.as_dict()
+        assert p.partial_bytes == 2048 * 63 * 1024 + 8 * 2048 < H * W * 12 * 63 // 40
 
 
 def test_bench_two_ranks_rehearsal(tmp_path):
@@ -835,3 +895,17 @@ def test_numerics_helpers_match_ieee():
         assert out[3] == 1 << 24
         assert (out[0], out[1], out[2], out[4]) == (0, 0, 0, 0), (list(out), list(ex))
 
+
+
+def test_library_before_torch_keeps_one_hip_runtime():
+    """Loading the library before torch must leave torch's device usable (one HIP runtime per
+    process: rtgpu loads torch's first; the other order made torch report "No HIP GPUs")."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r); import rtgpu; L = rtgpu.Library(); "
+            "assert L.device_count() >= 1; import torch; torch.cuda.init(); "
+            "x = torch.ones(4, device='cuda'); print(float(x.sum()))"
+            % os.path.join(REPO, "raytracing-practice_amd", "python"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("4.0"), r.stderr[-2000:]

@@ -233,6 +233,8 @@ Knobs read_knobs() {
   if (num("RTG_STACK", 16, 64, &st) && (st == 16 || st == 32 || st == 64)) k.stack = st;
   int ts = 0;  // tile-ring slots: 0 or a power of two (tests shrink the ring to force slot waits)
   if (num("RTG_TILE_SLOTS", 0, 65536, &ts) && (ts & (ts - 1)) == 0) k.tile_slots = ts;
+  num("RTG_TREELET_STACK", 4, 16, &k.treelet_stack);
+  num("RTG_TREELET_HOT", 0, 1, &k.treelet_hot);
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -709,6 +711,11 @@ struct rtg_scene {
   size_t dev_out_bytes = 0;
   float* pending_host_out = nullptr;
   size_t pending_host_bytes = 0;
+  // hot treelet (schedule 5): the node array is renumbered so the nodes a probe render of this
+  // camera visited most come first, i.e. into the LDS prefix (tune_treelet); key of that camera
+  uint64_t treelet_key = 0;
+  uint32_t* probe_visits = nullptr;  // set only while the probe render runs
+  double treelet_tune_ms = 0.0;
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
@@ -1125,8 +1132,10 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   // most its occupancy allows), deeper BVHs spill the rest to a global per-wave area; the A/B
   // schedules 1 and 2 keep the whole stack in LDS.
   const int need = std::max(1, s->stack_need);
+  int treelet_entries = kLdsStack;  // LDS stack entries per lane of the treelet schedule
   DevScene& dscene = P->dscene;
   dscene = s->dev;         // this render's view (the treelet schedule sets its LDS part)
+  dscene.node_visits = P->count ? s->probe_visits : nullptr;  // the hot-treelet probe only
   dj.lds_sphere_f4 = 3;    // 48-B sphere records in LDS (bank spread)
   // persistent LDS schedule, by scene size (DESIGN.md §3 "occupancy"): five 4-wave workgroups per CU
   // when five copies of scene + stacks fit one CU's LDS (5 waves per SIMD at <= 96 VGPRs; Cornell
@@ -1183,7 +1192,9 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     if (dscene.node_width != 4) return fail(RTG_E_INVALID, "schedule 5 needs a 4-wide BVH (RTG_BVH_SAH)");
     dj.stack_esz = 4;
     dj.lds_waves = kLdsWaves;
-    lds_bytes = lds_layout_treelet(&dscene, kLdsStack, kLdsWaves, &dj);
+    // LDS stack entries: trees that spill anyway may keep fewer of them in LDS and more treelet nodes
+    treelet_entries = need > kLdsStack && !lds_entries_knob ? K.treelet_stack : kLdsStack;
+    lds_bytes = lds_layout_treelet(&dscene, treelet_entries, kLdsWaves, &dj);
     if (lds_bytes < 0) return fail(RTG_E_INVALID, "schedule 5: no LDS room for the treelet");
   }
   if (variant == 4) variant = 0;  // plain-grid ballot schedule
@@ -1214,6 +1225,7 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   dj.lds_stack = stack_depth;
   // RTG_STACK_LDS_ENTRIES (tests): keep fewer entries in LDS so the global spill path is exercised
   if (lds_entries_knob) dj.lds_stack = std::min(stack_depth, K.stack_lds_entries);
+  if (variant == 5) dj.lds_stack = std::min(dj.lds_stack, treelet_entries);
   P->default_sched = variant == 3 || variant == 0 || variant == 5;  // the ballot-batched stream
   dj.spill_depth = P->default_sched ? std::max(0, need - dj.lds_stack) : 0;
   if (P->progressive && !P->default_sched)
@@ -1273,6 +1285,100 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   return RTG_OK;
 }
 
+// The camera (and shard rows) a hot treelet was tuned for.
+uint64_t treelet_key(const rtg_camera_desc* c, const rtg_render_desc* j) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t k = 0; k < n; ++k) h = (h ^ b[k]) * 1099511628211ull;
+  };
+  const double d[] = {c->aspect_ratio, c->vfov, c->lookfrom[0], c->lookfrom[1], c->lookfrom[2], c->lookat[0],
+                      c->lookat[1],    c->lookat[2], c->vup[0],   c->vup[1],    c->vup[2],    c->defocus_angle,
+                      c->focus_dist};
+  const int32_t i[] = {c->image_width, c->max_depth, j->row_begin, j->row_stride};
+  mix(d, sizeof(d));
+  mix(i, sizeof(i));
+  return h | 1;  // never 0 (0: not tuned)
+}
+
+// Hot treelet (schedule 5, scenes whose tree does not fit LDS): the persistent workgroups keep the
+// first treelet_bytes of the node array in LDS, so which nodes come first decides which visits are
+// ds_reads. A probe render of this camera (1 sample per pixel on every 4th row of the shard, the
+// counting kernel with one counter per node) counts the visits of every node; the node array is then
+// renumbered on the host, the root first, the others by visits (ties and unvisited nodes in their
+// previous order), and uploaded again. Traversal order and the frame are unchanged (same tree, same
+// child slots); only where a node is read from changes. Runs on the first render of a camera.
+rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, uint64_t key) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t n = s->dev.num_nodes;
+  s->treelet_key = key;  // tuned or not, a failed probe is not retried for this camera
+  if (n <= 1 || n > (int64_t(1) << 24)) return RTG_OK;
+  rtg_camera_desc c2 = *cam;
+  c2.samples_per_pixel = 1;
+  rtg_render_desc j2 = *job;
+  j2.flags = RTG_RENDER_COUNT | RTG_RENDER_OUT_DEVICE | (5 << 8);
+  j2.row_stride = job->row_stride * 4;
+  j2.row_count = 0;
+  j2.partial = nullptr;
+  j2.chunk_begin = j2.chunk_count = 0;
+  j2.stream = nullptr;
+  rtg_camera_params cp;
+  resolve_camera(&c2, &cp);
+  const int64_t rows = (cp.image_height - 1 - j2.row_begin) / j2.row_stride + 1;
+  uint32_t* visits = nullptr;
+  float* out = nullptr;
+  RTG_HIP(hipMalloc(reinterpret_cast<void**>(&visits), n * 4), "hipMalloc(node visits)");
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&out), rows * cp.image_width * 12);
+  // the probe runs on the scene's own (non-blocking) stream: every copy here is ordered on it
+  hipStream_t os = s->own_stream;
+  if (e == hipSuccess) e = hipMemsetAsync(visits, 0, n * 4, os);
+  rtg_status st = e == hipSuccess ? RTG_OK : hip_fail(e, "hot treelet probe buffers");
+  if (st == RTG_OK) {
+    s->probe_visits = visits;
+    rtg_render_stats ps{};
+    st = rtg_render(s, &c2, &j2, out, &ps);
+    s->probe_visits = nullptr;
+  }
+  std::vector<uint32_t> cnt;
+  std::vector<int32_t> rec;
+  if (st == RTG_OK) {
+    cnt.resize(n);
+    rec.resize(n * 28);
+    e = hipMemcpyAsync(cnt.data(), visits, n * 4, hipMemcpyDeviceToHost, os);
+    if (e == hipSuccess) e = hipMemcpyAsync(rec.data(), s->dev.nodes, n * 112, hipMemcpyDeviceToHost, os);
+    if (e == hipSuccess) e = hipStreamSynchronize(os);
+    if (e != hipSuccess) st = hip_fail(e, "hot treelet download");
+  }
+  (void)hipFree(out);
+  (void)hipFree(visits);
+  if (st != RTG_OK) return st;
+  std::vector<int32_t> order(n);
+  for (int64_t k = 0; k < n; ++k) order[k] = static_cast<int32_t>(k);
+  std::stable_sort(order.begin() + 1, order.end(), [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
+  std::vector<int32_t> pos(n);
+  for (int64_t k = 0; k < n; ++k) pos[order[k]] = static_cast<int32_t>(k);
+  std::vector<int32_t> out_rec(n * 28);
+  for (int64_t k = 0; k < n; ++k) {
+    std::memcpy(&out_rec[k * 28], &rec[static_cast<int64_t>(order[k]) * 28], 112);
+    int32_t* code = &out_rec[k * 28 + 24];
+    for (int c = 0; c < 4; ++c)
+      if (code[c] >= 0) code[c] = pos[code[c] / 112] * 112;  // inner child: byte offset of its node
+  }
+  e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), out_rec.data(), n * 112, hipMemcpyHostToDevice, os);
+  if (e == hipSuccess) e = hipStreamSynchronize(os);
+  if (e != hipSuccess) return hip_fail(e, "hot treelet upload");
+  s->treelet_tune_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (s->knobs.verbose) {
+    uint64_t total = 0, top = 0;
+    for (int64_t k = 0; k < n; ++k) total += cnt[k];
+    for (int64_t k = 0; k < std::min<int64_t>(n, 877); ++k) top += cnt[order[k]];
+    std::fprintf(stderr, "[rtg] hot treelet: %.1f ms, probe %lld rows, %llu node visits, first 877 nodes %.1f %%\n",
+                 s->treelet_tune_ms, static_cast<long long>(rows), static_cast<unsigned long long>(total),
+                 total ? 100.0 * top / total : 0.0);
+  }
+  return RTG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1326,6 +1432,18 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   rtg_status pst = plan_render(s, cam, job, &P);
   if (pst != RTG_OK) return pst;
   const Knobs& K = s->knobs;
+  if (P.variant == 5 && !P.count && K.treelet_hot && s->dev.node_width == 4) {
+    const uint64_t key = treelet_key(cam, job);
+    if (key != s->treelet_key) {  // first render of this camera: probe, renumber, plan again
+      RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+      if (job->stream) RTG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(job->stream)), "stream sync");
+      pst = tune_treelet(s, cam, job, key);
+      if (pst != RTG_OK) return pst;
+      P = Plan{};
+      pst = plan_render(s, cam, job, &P);
+      if (pst != RTG_OK) return pst;
+    }
+  }
   const int W = P.W, rows = P.rows;
   DevJob& dj = P.dj;
   DevJob& j4 = P.j4;

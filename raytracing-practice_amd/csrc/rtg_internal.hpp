@@ -155,6 +155,9 @@ struct DevScene {
   int32_t treelet_bytes;
   uint32_t treelet_lds;  // LDS byte address of that copy (set inside the kernel)
   int32_t sphere_f4;     // float4s per sphere record: 2 in HBM, DevJob::lds_sphere_f4 in the LDS copy
+  // counting renders of the cache-read schedules: per-node visit counters (node index = code / 112),
+  // the probe behind the hot treelet (rtg_api.cpp tune_treelet); null otherwise
+  uint32_t* node_visits;
 };
 
 // A render kernel picked for a plan (rtg_kernels.hip choose_kernel); fn == nullptr: none fits.
@@ -210,6 +213,10 @@ struct Knobs {
   int dual = -1;                // RTG_DUAL 0 | 1 (-1: where it fits)
   int stack = 0;                // RTG_STACK 16 | 32 | 64 (A/B schedules only)
   int tile_slots = -1;          // RTG_TILE_SLOTS 0 (full-frame partials) | 1..65536 (-1: by chunks)
+  int treelet_stack = 16;       // RTG_TREELET_STACK 4..16: LDS stack entries of the treelet schedule
+                                // (fewer: more treelet nodes, more spill traffic; spilling trees only)
+  int treelet_hot = 1;          // RTG_TREELET_HOT 0 | 1: treelet of the most-visited nodes for the
+                                // camera (a probe render counts node visits), 0: breadth-first top
   std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
 };
 Knobs read_knobs();

@@ -412,6 +412,8 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
     t.todo = kTravDone;
     return;
   }
+  // the probe of the hot treelet counts every visit of a node held in HBM (rtg_api.cpp tune_treelet)
+  if (COUNT && GEOM != kGeomLds && S.node_visits) atomicAdd(S.node_visits + t.todo / 112, 1u);
   const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
   const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
   const uint32_t na = static_cast<uint32_t>(t.todo);  // LDS scenes: the node's LDS address
@@ -1351,7 +1353,10 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
       // overhead, and a lane's second step overlaps the other lanes' load latency), 1 for LDS scenes
       // (2: neutral, 3: +3 %)
-      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : 2;
+#ifndef RTG_AB_CACHE_NODE_REPS
+#define RTG_AB_CACHE_NODE_REPS 2
+#endif
+      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : RTG_AB_CACHE_NODE_REPS;
 #pragma unroll
       for (int rep = 0; rep < kNodeReps; ++rep) {
         if (at_inner(tr)) {
@@ -1499,8 +1504,11 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
                     static_cast<uint32_t>(J.lds_nodes);
     WaveStats<COUNT> w;
     if constexpr (SPILL) {
+      // the LDS part of a spilling stack is J.lds_stack (<= STACK) entries per lane: the host may keep
+      // fewer than STACK there to leave the treelet more room (RTG_TREELET_STACK)
       const int slot = blockIdx.x * wpb + wave;
-      const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
+      int32_t* tstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * J.lds_stack * 64 + lane;
+      const SpillStack<STACK> stk{tstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                   J.lds_stack, J.lds_stack + J.spill_depth};
       render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, stk, w, rtab);
     } else {

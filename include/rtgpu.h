@@ -295,11 +295,26 @@ typedef struct rtg_launch_plan {
   int32_t num_cus;
   int32_t tile_slots;        /* > 0: chunks are summed per tile through a ring of this many tile
                                 slots (partial_bytes = ring + slot words); 0: full-frame partials */
-  int32_t reserved_[6];
+  int32_t treelet_hot;       /* schedule 5: 1 when the node array is ordered for this camera (the
+                                most-visited nodes are the treelet; rtg_scene_prepare), 0: not yet */
+  int32_t treelet_tune_us;   /* host + probe time of the scene's last hot-treelet tuning */
+  int32_t reserved_[4];
 } rtg_launch_plan;
 
 rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,
                            rtg_launch_plan* out);
+
+/* Optional setup before the first render of a camera (and shard rows) on a scene (ABI 5 addition).
+ * Scenes whose BVH does not fit LDS render with the treelet schedule, which keeps a prefix of the
+ * 4-wide node array in each workgroup's LDS; here a probe render (1 sample per pixel on every 4th
+ * row of the shard, counting kernel) counts every node's visits for this camera and the node array
+ * is renumbered so the most-visited nodes form that prefix (the "hot treelet"; the root stays first).
+ * Traversal order and frames are unchanged: only where a node is read from changes. rtg_render does
+ * the same on its first render of a camera; calling this first keeps the probe (~0.3 s for 1M
+ * spheres at 4K) out of that render. A no-op for every other schedule and with RTG_TREELET_HOT=0.
+ * Not concurrent with renders of the same scene (it rewrites the scene's node array). No reference
+ * counterpart: the reference's bvh_node keeps its nodes in host memory (bvh_node.hpp:25-77). */
+rtg_status rtg_scene_prepare(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job);
 
 /* write_color (color.hpp:26-58) on the device: gamma 2, clamp [0, 0.999], int(256*x).
  * in_rgb / out_rgb8 are device pointers on the scene's device; n_pixels pixels. */

@@ -1301,6 +1301,11 @@ uint64_t treelet_key(const rtg_camera_desc* c, const rtg_render_desc* j) {
   return h | 1;  // never 0 (0: not tuned)
 }
 
+bool wants_treelet_tune(const rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, const Plan& P) {
+  return P.variant == 5 && !P.count && s->knobs.treelet_hot && s->dev.node_width == 4 &&
+         treelet_key(cam, job) != s->treelet_key;
+}
+
 // Hot treelet (schedule 5, scenes whose tree does not fit LDS): the persistent workgroups keep the
 // first treelet_bytes of the node array in LDS, so which nodes come first decides which visits are
 // ds_reads. A probe render of this camera (1 sample per pixel on every 4th row of the shard, the
@@ -1420,7 +1425,24 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
                                                      : static_cast<int64_t>(P.out_bytes) * P.dj.chunks;
   out->tile_slots = P.ring_slots;
   out->num_cus = s->num_cus;
+  if (P.variant == 5) {
+    out->treelet_hot = s->treelet_key == treelet_key(cam, job) ? 1 : 0;
+    out->treelet_tune_us = static_cast<int32_t>(std::min(s->treelet_tune_ms * 1e3, 2e9));
+  }
   return RTG_OK;
+}
+
+rtg_status rtg_scene_prepare(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job) {
+  if (!s || !cam || !job) return fail(RTG_E_INVALID, "null argument");
+  if (s->pending) return fail(RTG_E_INVALID, "a previous async render was not waited for");
+  Plan P;
+  const rtg_status pst = plan_render(s, cam, job, &P);
+  if (pst != RTG_OK) return pst;
+  if (!wants_treelet_tune(s, cam, job, P)) return RTG_OK;
+  RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+  // renders still in flight on the caller's stream read the node array this renumbers
+  if (job->stream) RTG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(job->stream)), "stream sync");
+  return tune_treelet(s, cam, job, treelet_key(cam, job));
 }
 
 rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,
@@ -1432,17 +1454,12 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   rtg_status pst = plan_render(s, cam, job, &P);
   if (pst != RTG_OK) return pst;
   const Knobs& K = s->knobs;
-  if (P.variant == 5 && !P.count && K.treelet_hot && s->dev.node_width == 4) {
-    const uint64_t key = treelet_key(cam, job);
-    if (key != s->treelet_key) {  // first render of this camera: probe, renumber, plan again
-      RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
-      if (job->stream) RTG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(job->stream)), "stream sync");
-      pst = tune_treelet(s, cam, job, key);
-      if (pst != RTG_OK) return pst;
-      P = Plan{};
-      pst = plan_render(s, cam, job, &P);
-      if (pst != RTG_OK) return pst;
-    }
+  if (wants_treelet_tune(s, cam, job, P)) {  // first render of this camera: probe, renumber, plan again
+    pst = rtg_scene_prepare(s, cam, job);
+    if (pst != RTG_OK) return pst;
+    P = Plan{};
+    pst = plan_render(s, cam, job, &P);
+    if (pst != RTG_OK) return pst;
   }
   const int W = P.W, rows = P.rows;
   DevJob& dj = P.dj;

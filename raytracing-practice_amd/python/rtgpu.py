@@ -116,7 +116,8 @@ class rtg_launch_plan(C.Structure):
         "waves_per_simd", "dual", "dual_workgroups", "dual_lds_bytes", "dual_vgprs", "stack_entry_bytes",
         "lds_stack_entries", "spill_entries", "treelet_nodes", "shade_batch", "leaf_batch", "chunk_samples",
         "chunks")] + [("partial_bytes", C.c_int64), ("num_cus", C.c_int32), ("tile_slots", C.c_int32),
-                      ("reserved_", C.c_int32 * 6)]
+                      ("treelet_hot", C.c_int32), ("treelet_tune_us", C.c_int32),
+                      ("reserved_", C.c_int32 * 4)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved_"}
@@ -139,7 +140,7 @@ RTG_SYMBOLS = ("rtg_abi_version", "rtg_last_error", "rtg_device_count", "rtg_cam
                "rtg_render_wait", "rtg_resolve_rgb8", "rtg_bvh_build_host", "rtg_comm_create_local",
                "rtg_comm_unique_id", "rtg_comm_create_rank", "rtg_comm_size", "rtg_comm_destroy",
                "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame", "rtg_render_plan",
-               "rtg_shard_layout", "rtg_deinterleave_rows_host")
+               "rtg_shard_layout", "rtg_deinterleave_rows_host", "rtg_scene_prepare")
 RTG_COMM_ID_BYTES = 128
 
 
@@ -217,6 +218,7 @@ class Library:
         L.rtg_render_frame.argtypes = [C.c_void_p, _P(C.c_void_p), _P(rtg_camera_desc), C.c_uint64, C.c_int32,
                                        C.c_void_p, _P(rtg_render_stats)]
         L.rtg_render_plan.argtypes = [C.c_void_p, _P(rtg_camera_desc), _P(rtg_render_desc), _P(rtg_launch_plan)]
+        L.rtg_scene_prepare.argtypes = [C.c_void_p, _P(rtg_camera_desc), _P(rtg_render_desc)]
         L.rtg_shard_layout.argtypes = [C.c_int32, C.c_int32, C.c_int32] + [_P(C.c_int32)] * 4
         L.rtg_deinterleave_rows_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64]
         for name in ("rtg_device_count", "rtg_camera_resolve", "rtg_scene_create",
@@ -385,6 +387,13 @@ class DeviceScene:
         self.L.check("rtg_render_plan", self.L.lib.rtg_render_plan(self.handle, C.byref(cam), C.byref(job),
                                                                     C.byref(out)))
         return out
+
+    def prepare(self, cam: rtg_camera_desc, row_begin: int = 0, row_stride: int = 1, row_count: int = 0,
+                stream=None):
+        """rtg_scene_prepare: the setup the first render of this camera would do (the hot treelet of
+        scenes that render with the treelet schedule; a no-op otherwise)."""
+        job = rtg_render_desc(DEFAULT_SEED, row_begin, row_stride, row_count, RTG_RENDER_OUT_DEVICE, stream)
+        self.L.check("rtg_scene_prepare", self.L.lib.rtg_scene_prepare(self.handle, C.byref(cam), C.byref(job)))
 
     def render_host(self, cam: rtg_camera_desc, seed: int = DEFAULT_SEED, row_begin: int = 0,
                     row_stride: int = 1, row_count: int = 0, count: bool = False):

@@ -258,6 +258,48 @@ def test_treelet_schedule_matches_default(gpu_lib, scenes, oracle, grid, W, monk
     assert_parity(ref, o, rst, segs)
 
 
+def test_hot_treelet_keeps_the_frame(gpu_lib, scenes, oracle, monkeypatch):
+    """Hot treelet (rtg_scene_prepare): a probe render counts node visits for the camera
+    and the node array is renumbered so the most-visited nodes form the LDS prefix of the treelet
+    schedule. Same tree, same child slots: the frame and the segment count equal the breadth-first
+    treelet's and the plain grid's, bit for bit, on the 1M-sphere scene (whose tree is ~1500x the
+    treelet); the plan reports the tuning; a scene that fits LDS (book-1) is left alone."""
+    s = scenes.build("bouncing_spheres", grid=500, rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.aspect_ratio, c.samples_per_pixel, c.max_depth = 160, 16.0 / 9.0, 8, 50
+    monkeypatch.setenv("RTG_TREELET_HOT", "0")
+    ds = gpu_lib.scene_create(s.desc)  # knobs are read once per scene
+    monkeypatch.delenv("RTG_TREELET_HOT")
+    bfs, bst = ds.render_host(c)
+    assert ds.plan(c).treelet_hot == 0
+    ds.close()
+    ds = gpu_lib.scene_create(s.desc)
+    p0 = ds.plan(c)
+    assert (p0.schedule, p0.treelet_hot) == (5, 0), p0.as_dict()
+    ds.prepare(c)
+    p1 = ds.plan(c)
+    assert p1.treelet_hot == 1 and p1.treelet_tune_us > 0, p1.as_dict()
+    hot, hst = ds.render_host(c)
+    assert np.array_equal(hot, bfs) and hst.segments == bst.segments
+    # another camera (here: other rows) is not the tuned one until its first render re-tunes
+    c2 = rtgpu.rtg_camera_desc.from_buffer_copy(c)
+    c2.lookfrom[0] += 3.0
+    assert ds.plan(c2).treelet_hot == 0
+    hot2, st2 = ds.render_host(c2)
+    assert ds.plan(c2).treelet_hot == 1 and ds.plan(c).treelet_hot == 0
+    ds.close()
+    o, segs = oracle.render_f32(s.desc, c2)
+    assert_parity(hot2, o, st2, segs)
+    b = scenes.build("bouncing_spheres", grid=11, rand_seed=1)
+    cb = rtgpu.rtg_camera_desc.from_buffer_copy(b.camera)
+    cb.image_width, cb.samples_per_pixel = 96, 4
+    db = gpu_lib.scene_create(b.desc)
+    db.prepare(cb)
+    pb = db.plan(cb)
+    db.close()
+    assert pb.schedule == 3 and pb.treelet_hot == 0 and pb.treelet_tune_us == 0
+
+
 def test_repeated_host_renders_are_identical(gpu_lib, scenes):
     """Host-output renders go through a scene-owned device frame and a pinned staging buffer; with
     a stream-ordered (hipMallocAsync) frame the third render of a scene came back all zero."""

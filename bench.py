@@ -498,6 +498,14 @@ def main():
             line["speedup_vs_cpu"] = round(line["value"] / cb["value"], 1) if cb["value"] else None
             line["speedup_vs_cpu_one_core"] = (round(line["value"] / cb["one_core"]["value"], 1)
                                                if cb["one_core"]["value"] else None)
+            # the same ratio against every CPU the host has online, extrapolated linearly from the
+            # one-core rate (the box's cgroup grants only cb["cores"] of them): an upper bound on what
+            # the whole host could do, next to the measured ratios
+            online = cb.get("host_cpus_online") or 0
+            if cb["one_core"]["value"] and online:
+                lin = cb["one_core"]["value"] * online
+                line["speedup_vs_cpu_all_host_cores_linear"] = {
+                    "cores": online, "cpu_value": round(lin, 1), "speedup": round(line["value"] / lin, 1)}
         if last_frame is not None:
             cores = host_cpus()[0]
             cb = line["cpu_baseline"]

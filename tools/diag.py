@@ -27,6 +27,7 @@ def main():
     s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
                                    spp=a.spp, max_depth=a.depth)
     ds = lib.scene_create(s.desc)
+    ds.prepare(s.camera)  # per-camera setup the bench does too (the hot treelet of schedule 5)
     out = {}
     out["lib"] = lib.path
     for b in [int(x) for x in a.batches.split(",")]:

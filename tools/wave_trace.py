@@ -37,12 +37,12 @@ def main():
     lib = rtgpu.Library(os.path.join(REPO, a.lib) if a.lib else None)
     s = rtgpu.SceneLibrary().build(a.scene, grid=a.grid, image_width=a.width, aspect_ratio=16.0 / 9.0,
                                    spp=a.spp, max_depth=a.depth)
+    path = os.path.join(tempfile.gettempdir(), f"rtg_trace_{os.getpid()}.bin")
+    os.environ["RTG_WAVE_TRACE"] = path  # knobs are read once, when the scene is created
     ds = lib.scene_create(s.desc)
     H = lib.camera_resolve(s.camera).image_height
     b, stride, cnt = rtgpu.shard_rows(H, 0, a.shard_of)
     buf = np.zeros((max(cnt, 1), a.width, 3), dtype=np.float32)
-    path = os.path.join(tempfile.gettempdir(), f"rtg_trace_{os.getpid()}.bin")
-    os.environ["RTG_WAVE_TRACE"] = path
     job = rtgpu.rtg_render_desc(0x5EED, b, stride, cnt if a.shard_of > 1 else 0, a.schedule << 8, None)
     st = rtgpu.rtg_render_stats()
     lib.check("rtg_render", lib.lib.rtg_render(ds.handle, C.byref(s.camera), C.byref(job), buf.ctypes.data,

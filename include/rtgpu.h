@@ -306,11 +306,11 @@ rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const r
 
 /* Optional setup before the first render of a camera (and shard rows) on a scene (ABI 5 addition).
  * Scenes whose BVH does not fit LDS render with the treelet schedule, which keeps a prefix of the
- * 4-wide node array in each workgroup's LDS; here a probe render (1 sample per pixel on every 4th
- * row of the shard, counting kernel) counts every node's visits for this camera and the node array
+ * 4-wide node array in each workgroup's LDS; here a probe render (1 sample per pixel on about 2^19
+ * pixels, every k-th row of the shard; counting kernel) counts every node's visits for this camera and the node array
  * is renumbered so the most-visited nodes form that prefix (the "hot treelet"; the root stays first).
  * Traversal order and frames are unchanged: only where a node is read from changes. rtg_render does
- * the same on its first render of a camera; calling this first keeps the probe (~0.3 s for 1M
+ * the same on its first render of a camera; calling this first keeps the probe (~0.2 s for 1M
  * spheres at 4K) out of that render. A no-op for every other schedule and with RTG_TREELET_HOT=0.
  * Not concurrent with renders of the same scene (it rewrites the scene's node array). No reference
  * counterpart: the reference's bvh_node keeps its nodes in host memory (bvh_node.hpp:25-77). */

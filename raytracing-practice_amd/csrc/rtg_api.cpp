@@ -1308,7 +1308,7 @@ bool wants_treelet_tune(const rtg_scene* s, const rtg_camera_desc* cam, const rt
 
 // Hot treelet (schedule 5, scenes whose tree does not fit LDS): the persistent workgroups keep the
 // first treelet_bytes of the node array in LDS, so which nodes come first decides which visits are
-// ds_reads. A probe render of this camera (1 sample per pixel on every 4th row of the shard, the
+// ds_reads. A probe render of this camera (1 sample per pixel on ~2^19 pixels: every k-th row of the shard, the
 // counting kernel with one counter per node) counts the visits of every node; the node array is then
 // renumbered on the host, the root first, the others by visits (ties and unvisited nodes in their
 // previous order), and uploaded again. Traversal order and the frame are unchanged (same tree, same
@@ -1322,7 +1322,13 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   c2.samples_per_pixel = 1;
   rtg_render_desc j2 = *job;
   j2.flags = RTG_RENDER_COUNT | RTG_RENDER_OUT_DEVICE | (5 << 8);
-  j2.row_stride = job->row_stride * 4;
+  {  // about 2^19 probe pixels: every k-th row of the shard (1080p: every 3rd, 4K: every 15th)
+    rtg_camera_params full;
+    resolve_camera(cam, &full);
+    const int64_t shard_rows = (full.image_height - 1 - job->row_begin) / job->row_stride + 1;
+    const int64_t k = std::max<int64_t>(1, std::min<int64_t>(64, (shard_rows * full.image_width) >> 19));
+    j2.row_stride = job->row_stride * static_cast<int32_t>(k);
+  }
   j2.row_count = 0;
   j2.partial = nullptr;
   j2.chunk_begin = j2.chunk_count = 0;

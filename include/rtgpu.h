@@ -316,6 +316,12 @@ rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const r
  * counterpart: the reference's bvh_node keeps its nodes in host memory (bvh_node.hpp:25-77). */
 rtg_status rtg_scene_prepare(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job);
 
+/* Host twin of the hot treelet's renumbering (tests; no device): num_nodes 4-wide nodes in the device
+ * record format (112 B each: 24 plane floats, then 4 int32 child codes; inner child = byte offset of
+ * its node, leaf < 0, empty INT32_MIN), renumbered in place so node 0 stays first and the others
+ * follow by descending visits[old index] (ties keep their order), inner codes remapped. */
+rtg_status rtg_hot_treelet_order_host(int32_t* nodes, const uint32_t* visits, int64_t num_nodes);
+
 /* write_color (color.hpp:26-58) on the device: gamma 2, clamp [0, 0.999], int(256*x).
  * in_rgb / out_rgb8 are device pointers on the scene's device; n_pixels pixels. */
 rtg_status rtg_resolve_rgb8(rtg_scene* scene, const float* in_rgb, uint8_t* out_rgb8,

@@ -1363,19 +1363,9 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   (void)hipFree(out);
   (void)hipFree(visits);
   if (st != RTG_OK) return st;
-  std::vector<int32_t> order(n);
-  for (int64_t k = 0; k < n; ++k) order[k] = static_cast<int32_t>(k);
-  std::stable_sort(order.begin() + 1, order.end(), [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
-  std::vector<int32_t> pos(n);
-  for (int64_t k = 0; k < n; ++k) pos[order[k]] = static_cast<int32_t>(k);
-  std::vector<int32_t> out_rec(n * 28);
-  for (int64_t k = 0; k < n; ++k) {
-    std::memcpy(&out_rec[k * 28], &rec[static_cast<int64_t>(order[k]) * 28], 112);
-    int32_t* code = &out_rec[k * 28 + 24];
-    for (int c = 0; c < 4; ++c)
-      if (code[c] >= 0) code[c] = pos[code[c] / 112] * 112;  // inner child: byte offset of its node
-  }
-  e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), out_rec.data(), n * 112, hipMemcpyHostToDevice, os);
+  std::vector<int32_t> order;
+  hot_order_nodes4(rec.data(), cnt.data(), n, &order);
+  e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), rec.data(), n * 112, hipMemcpyHostToDevice, os);
   if (e == hipSuccess) e = hipStreamSynchronize(os);
   if (e != hipSuccess) return hip_fail(e, "hot treelet upload");
   s->treelet_tune_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1449,6 +1439,20 @@ rtg_status rtg_scene_prepare(rtg_scene* s, const rtg_camera_desc* cam, const rtg
   // renders still in flight on the caller's stream read the node array this renumbers
   if (job->stream) RTG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(job->stream)), "stream sync");
   return tune_treelet(s, cam, job, treelet_key(cam, job));
+}
+
+rtg_status rtg_hot_treelet_order_host(int32_t* nodes, const uint32_t* visits, int64_t num_nodes) {
+  if (num_nodes < 0 || (num_nodes > 0 && (!nodes || !visits))) return fail(RTG_E_INVALID, "null argument");
+  if (num_nodes > (int64_t(1) << 24)) return fail(RTG_E_INVALID, "num_nodes above 2^24");
+  for (int64_t k = 0; k < num_nodes; ++k)  // every inner code must name a node of the array
+    for (int c = 0; c < 4; ++c) {
+      const int32_t code = nodes[k * 28 + 24 + c];
+      if (code >= 0 && (code % 112 != 0 || code / 112 >= num_nodes))
+        return fail(RTG_E_INVALID, "inner child code outside the node array");
+    }
+  std::vector<int32_t> order;
+  hot_order_nodes4(nodes, visits, num_nodes, &order);
+  return RTG_OK;
 }
 
 rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job,

@@ -12,6 +12,7 @@
 // leaves <= 4).
 #include <array>
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -830,6 +831,26 @@ void reorder_top_bfs(Bvh4* t, int64_t top) {
       if (out[k].child[c] >= 0) out[k].child[c] = pos[out[k].child[c]];
   }
   t->nodes.swap(out);
+}
+
+void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
+  std::vector<int32_t>& order = *order_out;
+  order.resize(n);
+  if (n <= 1) return;
+  for (int64_t k = 0; k < n; ++k) order[k] = static_cast<int32_t>(k);
+  // the root stays node 0 (DevScene::root_code); the others by visits, ties in their previous order
+  std::stable_sort(order.begin() + 1, order.end(),
+                   [&](int32_t a, int32_t b) { return visits[a] > visits[b]; });
+  std::vector<int32_t> pos(n);
+  for (int64_t k = 0; k < n; ++k) pos[order[k]] = static_cast<int32_t>(k);
+  std::vector<int32_t> out(static_cast<size_t>(n) * 28);
+  for (int64_t k = 0; k < n; ++k) {
+    std::memcpy(&out[k * 28], &rec[static_cast<int64_t>(order[k]) * 28], 112);
+    int32_t* code = &out[k * 28 + 24];
+    for (int c = 0; c < 4; ++c)
+      if (code[c] >= 0) code[c] = pos[code[c] / 112] * 112;  // inner child: byte offset of its node
+  }
+  std::memcpy(rec, out.data(), static_cast<size_t>(n) * 112);
 }
 
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {

@@ -91,6 +91,11 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm = Collap
 // that prefix in LDS (the treelet schedule), so the nodes every ray visits are ds_reads.
 constexpr int64_t kTreeletBfsNodes = 4096;
 void reorder_top_bfs(Bvh4* t, int64_t top);
+// Hot treelet (rtg_scene_prepare): renumber n device-format 4-wide nodes (112 B = 28 int32 each, codes
+// in the last 4: inner child = byte offset of its node) so the root stays first and the others follow
+// by descending visits (stable); inner codes remapped, leaf and empty codes unchanged. order_out[k] =
+// the old index of new node k.
+void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out);
 
 // aabb of one primitive exactly as the reference computes it (aabb.hpp:30-48,135-154;
 // sphere.hpp:16-44; quad.hpp:30-38).

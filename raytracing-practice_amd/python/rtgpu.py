@@ -140,7 +140,8 @@ RTG_SYMBOLS = ("rtg_abi_version", "rtg_last_error", "rtg_device_count", "rtg_cam
                "rtg_render_wait", "rtg_resolve_rgb8", "rtg_bvh_build_host", "rtg_comm_create_local",
                "rtg_comm_unique_id", "rtg_comm_create_rank", "rtg_comm_size", "rtg_comm_destroy",
                "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame", "rtg_render_plan",
-               "rtg_shard_layout", "rtg_deinterleave_rows_host", "rtg_scene_prepare")
+               "rtg_shard_layout", "rtg_deinterleave_rows_host", "rtg_scene_prepare",
+               "rtg_hot_treelet_order_host")
 RTG_COMM_ID_BYTES = 128
 
 
@@ -219,6 +220,7 @@ class Library:
                                        C.c_void_p, _P(rtg_render_stats)]
         L.rtg_render_plan.argtypes = [C.c_void_p, _P(rtg_camera_desc), _P(rtg_render_desc), _P(rtg_launch_plan)]
         L.rtg_scene_prepare.argtypes = [C.c_void_p, _P(rtg_camera_desc), _P(rtg_render_desc)]
+        L.rtg_hot_treelet_order_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.rtg_shard_layout.argtypes = [C.c_int32, C.c_int32, C.c_int32] + [_P(C.c_int32)] * 4
         L.rtg_deinterleave_rows_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64]
         for name in ("rtg_device_count", "rtg_camera_resolve", "rtg_scene_create",
@@ -286,6 +288,18 @@ class Library:
         v = [C.c_int32(0) for _ in range(4)]
         self.check("rtg_shard_layout", self.lib.rtg_shard_layout(height, nranks, rank, *[C.byref(x) for x in v]))
         return tuple(x.value for x in v)
+
+    def hot_treelet_order_host(self, nodes, visits):
+        """rtg_hot_treelet_order_host: a copy of `nodes` ((n, 28) int32 device-format 4-wide records)
+        renumbered as rtg_scene_prepare does (root first, then by descending visits)."""
+        import numpy as np
+
+        out = np.ascontiguousarray(nodes, dtype=np.int32).copy()
+        v = np.ascontiguousarray(visits, dtype=np.uint32)
+        assert out.ndim == 2 and out.shape[1] == 28 and v.shape == (out.shape[0],)
+        self.check("rtg_hot_treelet_order_host", self.lib.rtg_hot_treelet_order_host(
+            out.ctypes.data, v.ctypes.data, out.shape[0]))
+        return out
 
     def deinterleave_rows_host(self, gathered, nranks: int, height: int):
         """rtg_deinterleave_rows_host on a host array of nranks blocks of padded rows (row = last axes):

@@ -322,3 +322,50 @@ def test_parallel_sah_build_is_the_single_thread_tree(lib, scenes, monkeypatch):
             C.byref(d), nodes, nn.value, refs, nr.value, C.byref(nn), C.byref(nr), C.byref(depth)))
         trees[t] = (bytes(nodes), bytes(refs), depth.value)
     assert nn.value > 40000 and trees["1"] == trees["8"]
+
+
+def test_hot_treelet_order_keeps_the_tree(lib):
+    """rtg_hot_treelet_order_host, the host twin of rtg_scene_prepare's renumbering (DESIGN.md §3 "hot
+    treelet"): the root stays node 0, the others follow by descending visits (ties in their previous
+    order), inner child codes (byte offsets) are remapped, leaf and empty codes kept — so walking the
+    tree from the root reaches the same node records in the same slot order."""
+    rng = np.random.default_rng(7)
+    n = 300
+    nodes = np.zeros((n, 28), dtype=np.int32)
+    nodes[:, :24] = rng.integers(-2**20, 2**20, size=(n, 24))  # plane payload: just carried along
+    nodes[:, 24:] = np.iinfo(np.int32).min                      # empty slots
+    nxt = 1
+    for k in range(n):  # a random 4-wide tree in depth-first-ish order, leaves as negative codes
+        for c in range(rng.integers(1, 5)):
+            if k < nxt < n and rng.random() < 0.8:  # children after their parent: no cycles
+                nodes[k, 24 + c] = nxt * 112
+                nxt += 1
+            else:
+                nodes[k, 24 + c] = ~((int(rng.integers(0, 4096)) << 3) | int(rng.integers(0, 4)))
+    assert nxt == n
+    visits = rng.integers(0, 50, size=n).astype(np.uint32)
+    visits[0] = 7  # the root keeps index 0 whatever its count
+    out = lib.hot_treelet_order_host(nodes, visits)
+    order = sorted(range(1, n), key=lambda k: -int(visits[k]))  # Python's sort is stable
+    assert (out[0, :24] == nodes[0, :24]).all()
+    for new, old in enumerate([0] + order):
+        assert (out[new, :24] == nodes[old, :24]).all()
+
+    def walk(a, k, acc):
+        acc.append(tuple(a[k, :24]))
+        for c in range(4):
+            code = int(a[k, 24 + c])
+            if code >= 0:
+                assert code % 112 == 0
+                walk(a, code // 112, acc)
+            else:
+                acc.append(code)
+        return acc
+
+    import sys
+    sys.setrecursionlimit(10000)
+    assert walk(out, 0, []) == walk(nodes, 0, [])
+    bad = nodes.copy()
+    bad[5, 24] = n * 112  # a code past the array is rejected, nothing renumbered
+    with pytest.raises(rtgpu.RtgError):
+        lib.hot_treelet_order_host(bad, visits)

@@ -43,6 +43,8 @@ HYBRID_RENDERS = [
     ("perlin", 64, 36, 4, 10, 7),
     ("earth", 64, 36, 4, 10, 11),  # image_texture on the committed texels (texture.hpp:91-122)
     ("earth_perlin", 64, 36, 4, 20, 13),  # BASELINE config 3's scene
+    ("checkered", 64, 36, 8, 20, 17),  # checkered_spheres (main.cpp:104-138)
+    ("quads", 40, 40, 8, 50, 19),  # quads (main.cpp:210-251)
 ]
 
 # G5: (scene, W, H, spp per process, processes, depth). book1 = BASELINE config-1
@@ -58,6 +60,8 @@ MOMENTS = [
     ("book1_g500", 96, 54, 256, 8, 50),
     ("earth_perlin", 192, 108, 512, 8, 50),  # BASELINE config 3's scene: image + noise textures
     ("earth", 128, 72, 512, 8, 50),
+    ("checkered", 128, 72, 512, 8, 20),  # the reference's own depth (main.cpp:122)
+    ("quads", 96, 96, 512, 8, 50),
 ]
 MOMENTS_SEED0 = 90001
 

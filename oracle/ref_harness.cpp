@@ -425,7 +425,10 @@ static void setup_cam(const std::string& scene, cam_t& c) {
     c.lookat = point3(0.0f, 2.0f, 0.0f);
   } else if (scene == "earth") {  // main.cpp:157-166
     c.lookfrom = point3(0.0f, 0.0f, 12.0f);
-  }  // earth_perlin (BASELINE config 3): perlin_sphere's camera, main.cpp:190-201
+  } else if (scene == "quads") {  // main.cpp:234-246
+    c.vfov = 80.0f;
+    c.lookfrom = point3(0.0f, 0.0f, 9.0f);
+  }  // earth_perlin (BASELINE config 3): perlin_sphere's camera, main.cpp:190-201; checkered: main.cpp:118-134
 }
 
 static std::shared_ptr<hittable> make_world(const std::string& scene) {
@@ -467,6 +470,21 @@ static std::shared_ptr<hittable> make_world(const std::string& scene) {
     w->add(std::make_shared<sphere>(point3(0.0f, -1000.0f, 0.0f), 1000.0f, std::make_shared<lambertian>(pertext)));
     auto globe = std::make_shared<lambertian>(std::make_shared<image_texture>(earthmap_path()));
     w->add(std::make_shared<sphere>(point3(0.0f, 2.0f, 0.0f), 2.0f, globe));
+  } else if (scene == "checkered") {  // main.cpp:104-116
+    auto checker = std::make_shared<checker_texture>(0.32f, color(0.2f, 0.3f, 0.1f), color(0.9f, 0.9f, 0.9f));
+    w->add(std::make_shared<sphere>(point3(0.0f, -10.0f, 0.0f), 10.0f, std::make_shared<lambertian>(checker)));
+    w->add(std::make_shared<sphere>(point3(0.0f, 10.0f, 0.0f), 10.0f, std::make_shared<lambertian>(checker)));
+  } else if (scene == "quads") {  // main.cpp:210-225
+    auto left_red = std::make_shared<lambertian>(color(1.0f, 0.2f, 0.2f));
+    auto back_green = std::make_shared<lambertian>(color(0.2f, 1.0f, 0.2f));
+    auto right_blue = std::make_shared<lambertian>(color(0.2f, 0.2f, 1.0f));
+    auto upper_orange = std::make_shared<lambertian>(color(1.0f, 0.5f, 0.0f));
+    auto lower_teal = std::make_shared<lambertian>(color(0.2f, 0.8f, 0.8f));
+    w->add(std::make_shared<quad>(point3(-3.0f, -2.0f, 5.0f), vec3(0.0f, 0.0f, -4.0f), vec3(0.0f, 4.0f, 0.0f), left_red));
+    w->add(std::make_shared<quad>(point3(-2.0f, -2.0f, 0.0f), vec3(4.0f, 0.0f, 0.0f), vec3(0.0f, 4.0f, 0.0f), back_green));
+    w->add(std::make_shared<quad>(point3(3.0f, -2.0f, 1.0f), vec3(0.0f, 0.0f, 4.0f), vec3(0.0f, 4.0f, 0.0f), right_blue));
+    w->add(std::make_shared<quad>(point3(-2.0f, 3.0f, 1.0f), vec3(4.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, 4.0f), upper_orange));
+    w->add(std::make_shared<quad>(point3(-2.0f, -3.0f, 5.0f), vec3(4.0f, 0.0f, 0.0f), vec3(0.0f, 0.0f, -4.0f), lower_teal));
   } else if (scene == "simple_light" || scene == "perlin") {  // main.cpp:174-207, 254-298
     auto pertext = std::make_shared<noise_texture>(4);
     w->add(std::make_shared<sphere>(point3(0.0f, -1000.0f, 0.0f), 1000.0f, std::make_shared<lambertian>(pertext)));

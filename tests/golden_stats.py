@@ -20,7 +20,7 @@ MOMENT_SCENES = {"book1": ("bouncing_spheres", 0), "cornell": ("cornell_box", 0)
                  "cornell_translate": ("cornell_translate", 0),
                  "simple_light": ("simple_light", 0), "perlin": ("perlin_sphere", 0),
                  "book1_g500": ("bouncing_spheres", 500), "earth_perlin": ("earth_perlin", 0),
-                 "earth": ("earth", 0)}
+                 "earth": ("earth", 0), "checkered": ("checkered_spheres", 0), "quads": ("quads", 0)}
 
 # numpy views of the C-ABI records (include/rtgpu.h)
 PRIM_DT = np.dtype([("kind", "<i4"), ("material", "<i4"), ("p0", "<f8", 3), ("p1", "<f8", 3),

@@ -38,7 +38,8 @@ def test_bouncing_spheres_grid_matches_reference(scenes, grid):
 
 
 @pytest.mark.parametrize("scene,spp", [("book1", 8), ("cornell", 16), ("cornell_translate", 16), ("simple_light", 8), ("perlin", 8),
-                                       ("book1_g500", 4), ("earth_perlin", 8), ("earth", 8)])
+                                       ("book1_g500", 4), ("earth_perlin", 8), ("earth", 8), ("checkered", 8),
+                                       ("quads", 8)])
 def test_cpu_ref32_statistical_parity_vs_reference(scenes, oracle, scene, spp):
     name, grid = MOMENT_SCENES[scene]
     s = scenes.build(name, grid=grid, rand_seed=1)

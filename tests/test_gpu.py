@@ -99,7 +99,8 @@ def test_depth100_scenes_match_oracle(gpu_lib, scenes, oracle, name, W, spp):
 # (tests/golden/moments_*.npz, >= 2048 samples per pixel of the ref-hybrid render from glibc rand()
 # streams). GPU samples per pixel: enough that 8x8-block means are gaussian.
 G5_GPU = [("book1", 1024), ("cornell", 2048), ("cornell_translate", 2048), ("simple_light", 1024),
-          ("perlin", 1024), ("book1_g500", 1024), ("earth_perlin", 1024), ("earth", 1024)]
+          ("perlin", 1024), ("book1_g500", 1024), ("earth_perlin", 1024), ("earth", 1024),
+          ("checkered", 1024), ("quads", 1024)]
 
 
 @pytest.mark.parametrize("scene,spp", G5_GPU)

@@ -18,7 +18,7 @@ from conftest import GOLDEN
 
 SCENE_OF = {"book1": "bouncing_spheres", "cornell": "cornell_box", "simple_light": "simple_light",
             "perlin": "perlin_sphere", "cornell_translate": "cornell_translate", "earth": "earth",
-            "earth_perlin": "earth_perlin"}
+            "earth_perlin": "earth_perlin", "checkered": "checkered_spheres", "quads": "quads"}
 
 
 def hybrid_camera(scene, W, H, spp, depth):
@@ -35,6 +35,8 @@ def hybrid_camera(scene, W, H, spp, depth):
         kw.update(background=(0, 0, 0), lookfrom=(26, 3, 6), lookat=(0, 2, 0))
     elif scene == "earth":
         kw.update(lookfrom=(0, 0, 12))
+    elif scene == "quads":
+        kw.update(vfov=80.0, lookfrom=(0, 0, 9))
     return rtgpu.camera(**kw)
 
 

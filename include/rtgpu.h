@@ -298,7 +298,9 @@ typedef struct rtg_launch_plan {
   int32_t treelet_hot;       /* schedule 5: 1 when the node array is ordered for this camera (the
                                 most-visited nodes are the treelet; rtg_scene_prepare), 0: not yet */
   int32_t treelet_tune_us;   /* host + probe time of the scene's last hot-treelet tuning */
-  int32_t reserved_[4];
+  int32_t treelet_visit_permille; /* treelet_hot: of the probe's node visits, the share (per mille)
+                                     that the treelet_nodes in LDS take */
+  int32_t reserved_[3];
 } rtg_launch_plan;
 
 rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,

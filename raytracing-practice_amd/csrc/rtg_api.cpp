@@ -716,6 +716,7 @@ struct rtg_scene {
   uint64_t treelet_key = 0;
   uint32_t* probe_visits = nullptr;  // set only while the probe render runs
   double treelet_tune_ms = 0.0;
+  std::vector<uint64_t> treelet_cum;  // probe visits of the first k nodes after the renumbering, k = 0..n
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
@@ -1369,10 +1370,10 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   if (e == hipSuccess) e = hipStreamSynchronize(os);
   if (e != hipSuccess) return hip_fail(e, "hot treelet upload");
   s->treelet_tune_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  s->treelet_cum.assign(n + 1, 0);
+  for (int64_t k = 0; k < n; ++k) s->treelet_cum[k + 1] = s->treelet_cum[k] + cnt[order[k]];
   if (s->knobs.verbose) {
-    uint64_t total = 0, top = 0;
-    for (int64_t k = 0; k < n; ++k) total += cnt[k];
-    for (int64_t k = 0; k < std::min<int64_t>(n, 877); ++k) top += cnt[order[k]];
+    const uint64_t total = s->treelet_cum[n], top = s->treelet_cum[std::min<int64_t>(n, 877)];
     std::fprintf(stderr, "[rtg] hot treelet: %.1f ms, probe %lld rows, %llu node visits, first 877 nodes %.1f %%\n",
                  s->treelet_tune_ms, static_cast<long long>(rows), static_cast<unsigned long long>(total),
                  total ? 100.0 * top / total : 0.0);
@@ -1424,6 +1425,11 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
   if (P.variant == 5) {
     out->treelet_hot = s->treelet_key == treelet_key(cam, job) ? 1 : 0;
     out->treelet_tune_us = static_cast<int32_t>(std::min(s->treelet_tune_ms * 1e3, 2e9));
+    const int64_t tn = P.dscene.treelet_bytes / 112;
+    if (out->treelet_hot && !s->treelet_cum.empty() && s->treelet_cum.back() > 0)
+      out->treelet_visit_permille = static_cast<int32_t>(
+          1000 * s->treelet_cum[std::min<int64_t>(tn, static_cast<int64_t>(s->treelet_cum.size()) - 1)] /
+          s->treelet_cum.back());
   }
   return RTG_OK;
 }

@@ -280,6 +280,7 @@ def test_hot_treelet_keeps_the_frame(gpu_lib, scenes, oracle, monkeypatch):
     ds.prepare(c)
     p1 = ds.plan(c)
     assert p1.treelet_hot == 1 and p1.treelet_tune_us > 0, p1.as_dict()
+    assert 500 < p1.treelet_visit_permille <= 1000, p1.as_dict()  # the LDS prefix takes most visits
     hot, hst = ds.render_host(c)
     assert np.array_equal(hot, bfs) and hst.segments == bst.segments
     # another camera (here: other rows) is not the tuned one until its first render re-tunes

@@ -715,6 +715,42 @@ static void sincos_turn(float u, float* sn, float* cs) {
   *sn = (qi >= 2) ? -s0 : s0;
 }
 
+/* The textures' transcendentals in the rtg-f32 spec (round 3; rtg_kernels.hip sin_spec / atan2_spec /
+   acos_spec, same operations in the same order): glibc's sinf / acosf / atan2f and the GPU's ocml
+   differ in the last ulp. sin: Cody-Waite reduction by pi/2 in three fmaf steps, Cephes' sinf / cosf
+   polynomials on [-pi/4, pi/4]; atan2: ratio of the smaller to the larger magnitude, shifted by pi/4
+   above tan(pi/8), Cephes' atanf polynomial, then the octant; acos v = atan2(sqrt(1 - v^2), v). */
+static float sin_spec(float x) {
+  float k = rintf(x * 0x1.45f306p-1f);
+  float r = fmaf(-k, 0x1.921fb6p+0f, x);
+  r = fmaf(-k, -0x1.777a5cp-25f, r);
+  r = fmaf(-k, -0x1.ee59dap-50f, r);
+  float z = r * r;
+  float sr = fmaf(fmaf(fmaf(-0x1.9943f2p-13f, z, 0x1.11073cp-7f), z, -0x1.555546p-3f) * z, r, r);
+  float cr = fmaf(fmaf(fmaf(0x1.99eb9cp-16f, z, -0x1.6c0c34p-10f), z, 0x1.55554ap-5f), z * z, fmaf(-0.5f, z, 1.0f));
+  int q = (int)k & 3;
+  float v = (q & 1) ? cr : sr;
+  return (q & 2) ? -v : v;
+}
+static float atan2_spec(float y, float x) {
+  float ax = fabsf(x), ay = fabsf(y);
+  float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  float a = mn > 0x1p-100f ? mn / mx : 0.0f;
+  int big = a > 0x1.a8279ap-2f;
+  float t = big ? (a - 1.0f) / (a + 1.0f) : a;
+  float z = t * t;
+  float r = fmaf(fmaf(fmaf(fmaf(0x1.49e1a2p-4f, z, -0x1.1c370ap-3f), z, 0x1.9924bep-3f), z, -0x1.555454p-2f) * z, t, t);
+  if (big) r = r + 0x1.921fb6p-1f;
+  if (ay > ax) r = 0x1.921fb6p+0f - r;
+  if (x < 0.0f) r = 0x1.921fb6p+1f - r;
+  return copysignf(r, y);
+}
+static float acos_spec(float v) { return atan2_spec(sqrtf(fmaxf(0.0f, fmaf(-v, v, 1.0f))), v); }
+/* exported for the accuracy check against libm (tests/test_oracle_parity.py) */
+float orc_sin_spec(float x) { return sin_spec(x); }
+float orc_atan2_spec(float y, float x) { return atan2_spec(y, x); }
+float orc_acos_spec(float v) { return acos_spec(v); }
+
 /* random_unit_vector (vec3.hpp:172-184), direct: z = 1 - 2U, then the azimuth from a second U */
 static f3 f32_random_unit_vector(uint64_t* s) {
   float z = 1.0f - 2.0f * U(s);
@@ -959,7 +995,7 @@ static f3 tex_value32(const world32* w, int32_t t, float u, float v, f3 p) {
         tp = fscl(2.0f, tp);
       }
       float tb = fabsf(accum);
-      float sv = 0.5f * (1.0f + sinf(fmaf(tf[0], p.z, 10.0f * tb)));
+      float sv = 0.5f * (1.0f + sin_spec(fmaf(tf[0], p.z, 10.0f * tb)));
       return F3(sv, sv, sv);
     }
     break;
@@ -1030,8 +1066,8 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
     int needs_uv = sphere && (m->type == RTG_MAT_LAMBERTIAN || m->type == RTG_MAT_DIFFUSE_LIGHT) &&
                    tex_uses_uv(w->s, m->texture, 0);
     if (needs_uv) {
-      float theta = acosf(-outward.y);
-      float phi = atan2f(-outward.z, outward.x) + 3.14159265358979323846f;
+      float theta = acos_spec(-outward.y);
+      float phi = atan2_spec(-outward.z, outward.x) + 3.14159265358979323846f;
       u = phi / (2.0f * 3.14159265358979323846f);
       v = theta / 3.14159265358979323846f;
     }

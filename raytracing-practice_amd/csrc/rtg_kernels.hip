@@ -111,6 +111,46 @@ __device__ __forceinline__ void sincos_turn(float u, float& sn, float& cs) {
   sn = (qi >= 2) ? -s0 : s0;
 }
 
+// The textures' transcendentals in the rtg-f32 spec (round 3). libm's sinf / acosf / atan2f (ocml
+// here, glibc in the oracle) differ in the last ulp, which left ~26 % of config 3's pixels off the
+// oracle by ~1e-6. These are fixed sequences of fp32 operations (fmaf, correctly rounded division and
+// square root, rint), restated in oracle/cpu_ref.c, so the GPU and the oracle agree to the bit.
+// sin: Cody-Waite reduction by pi/2 in three fmaf steps, then Cephes' sinf / cosf polynomials on
+// [-pi/4, pi/4] (about 1 ulp for |x| < 8192; the noise texture's argument is scale * z + 10 * turb).
+__device__ __forceinline__ float sin_spec(float x) {
+  const float k = rintf(x * 0x1.45f306p-1f);  // nearest multiple of pi/2
+  float r = fmaf(-k, 0x1.921fb6p+0f, x);
+  r = fmaf(-k, -0x1.777a5cp-25f, r);
+  r = fmaf(-k, -0x1.ee59dap-50f, r);
+  const float z = r * r;
+  const float sr = fmaf(fmaf(fmaf(-0x1.9943f2p-13f, z, 0x1.11073cp-7f), z, -0x1.555546p-3f) * z, r, r);
+  const float cr = fmaf(fmaf(fmaf(0x1.99eb9cp-16f, z, -0x1.6c0c34p-10f), z, 0x1.55554ap-5f), z * z,
+                        fmaf(-0.5f, z, 1.0f));
+  const int q = static_cast<int>(k) & 3;
+  const float v = (q & 1) ? cr : sr;
+  return (q & 2) ? -v : v;
+}
+// atan2: the ratio of the smaller to the larger magnitude, above tan(pi/8) shifted by pi/4, Cephes'
+// atanf polynomial, then the octant; the sign follows y (atan2(+-0, x >= +0) = +-0, x < 0: +-pi)
+__device__ __forceinline__ float atan2_spec(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float a = mn > 0x1p-100f ? div_rn(mn, mx) : 0.0f;  // div_rn's exact range (and atan ~ 0 below)
+  const bool big = a > 0x1.a8279ap-2f;  // tan(pi/8)
+  const float t = big ? div_rn(a - 1.0f, a + 1.0f) : a;
+  const float z = t * t;
+  float r = fmaf(fmaf(fmaf(fmaf(0x1.49e1a2p-4f, z, -0x1.1c370ap-3f), z, 0x1.9924bep-3f), z, -0x1.555454p-2f) * z,
+                 t, t);
+  if (big) r = r + 0x1.921fb6p-1f;      // + pi/4
+  if (ay > ax) r = 0x1.921fb6p+0f - r;  // pi/2 - r
+  if (x < 0.0f) r = 0x1.921fb6p+1f - r; // pi - r
+  return copysignf(r, y);
+}
+// acos v = atan2(sqrt(1 - v^2), v), v in [-1, 1]
+__device__ __forceinline__ float acos_spec(float v) {
+  return atan2_spec(sqrtf(fmaxf(0.0f, fmaf(-v, v, 1.0f))), v);
+}
+
 // random_unit_vector (vec3.hpp:172-184) by direct sampling (DESIGN.md rtg-f32): z = 1 - 2U, then
 // the azimuth from a second U. The reference's rejection loop would make every wave wait for its
 // unluckiest lane (~5 tries for 30 lanes at acceptance pi/6); this costs two draws, always.
@@ -763,7 +803,7 @@ __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3
       const float4* vec = S.perlin_vec + pt * 256;
       const int32_t* perm = S.perlin_perm + pt * 768;
       const float t = perlin_turb(vec, perm, p);
-      const float s = 0.5f * (1.0f + sinf(fmaf(t0.w, p.z, 10.0f * t)));
+      const float s = 0.5f * (1.0f + sin_spec(fmaf(t0.w, p.z, 10.0f * t)));
       return v3(s, s, s);
     }
     break;
@@ -849,8 +889,8 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
 
   // texture coordinates on spheres are only consumed by image textures
   auto sphere_uv = [&]() {
-    const float theta = acosf(-outward.y);
-    const float phi = atan2f(-outward.z, outward.x) + kPi;
+    const float theta = acos_spec(-outward.y);
+    const float phi = atan2_spec(-outward.z, outward.x) + kPi;
     u = div_rn(phi, 2.0f * kPi);
     v = div_rn(theta, kPi);
   };

@@ -48,10 +48,22 @@ class Oracle:
                                      C.c_int64, D3P]
         L.orc_bvh_replay.restype = C.c_int64
         L.orc_sincos_turn.argtypes = [C.c_float, P(C.c_float), P(C.c_float)]
+        for name, nargs in (("orc_sin_spec", 1), ("orc_atan2_spec", 2), ("orc_acos_spec", 1)):
+            getattr(L, name).argtypes = [C.c_float] * nargs
+            getattr(L, name).restype = C.c_float
         L.orc_f32_unit_vector.argtypes = [C.c_uint64, P(C.c_float)]
         L.orc_sphere_t32.argtypes = [P(C.c_float), P(C.c_float), P(C.c_float), C.c_float, C.c_float,
                                      C.c_float]
         L.orc_sphere_t32.restype = C.c_float
+
+    def sin_spec(self, x):
+        return self.lib.orc_sin_spec(x)
+
+    def atan2_spec(self, y, x):
+        return self.lib.orc_atan2_spec(y, x)
+
+    def acos_spec(self, v):
+        return self.lib.orc_acos_spec(v)
 
     def sincos_turn(self, u):
         sn, cs = C.c_float(), C.c_float()

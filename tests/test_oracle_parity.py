@@ -89,6 +89,28 @@ def test_cpu_ref32_path_length_matches_ref64(scenes, oracle, grid):
     assert abs(seg32 - seg64) / seg64 < 0.02, (seg32, seg64)
 
 
+def test_texture_transcendentals_are_accurate(oracle):
+    """The rtg-f32 spec's sin / atan2 / acos for the noise and image textures (DESIGN.md §4, round 3:
+    fixed fp32 sequences the GPU reproduces bit for bit, instead of libm's last-ulp-different sinf /
+    atan2f / acosf) stay within a few ulp of the true functions over the ranges the textures use."""
+    rng = np.random.default_rng(11)
+    xs = np.concatenate([rng.uniform(-8192, 8192, 4000), rng.uniform(-20, 20, 4000),
+                         np.arange(-64, 65) * np.float32(np.pi / 2)]).astype(np.float32)
+    err = max(abs(oracle.sin_spec(float(x)) - math.sin(float(x))) for x in xs)
+    assert err < 1.2e-7 + 0.0, err  # ~1 ulp of 1, plus the argument's own rounding near zeros
+    v = rng.normal(size=(6000, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    v = v.astype(np.float32)
+    pts = [(float(a), float(b)) for a, b in v[:, :2]] + [(0.0, 1.0), (0.0, -1.0), (1.0, 0.0), (-1.0, 0.0),
+                                                         (1e-30, -1.0), (-1e-30, -1.0), (3.0, 3.0)]
+    e2 = max(abs(oracle.atan2_spec(y, x) - math.atan2(y, x)) for y, x in pts)
+    assert e2 < 4e-7, e2
+    assert oracle.atan2_spec(0.0, -1.0) == np.float32(np.pi) and oracle.atan2_spec(-0.0, -1.0) == -np.float32(np.pi)
+    e3 = max(abs(oracle.acos_spec(float(y)) - math.acos(float(y))) for y in v[:, 1])
+    assert e3 < 5e-7, e3
+    assert oracle.acos_spec(1.0) == 0.0 and oracle.acos_spec(-1.0) == np.float32(np.pi)
+
+
 def test_direct_sampling_is_accurate_and_uniform(oracle):
     """rtg-f32 samples random_unit_vector / random_in_unit_disk directly with a
     libm-free sin/cos of 2*pi*u that the GPU reproduces bit for bit. It must be accurate (so the

@@ -3,8 +3,12 @@
 -> material::scatter) on the book-1 random-sphere scene, BASELINE config 2: 1920x1080, 500 spp,
 depth 50, on the MI355X kernels of librtgpu.so.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: starts its own N ranks, below)
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+Without a launcher, `--gpus N` (N > 1) starts `torch.distributed.run --nproc-per-node N` itself as a
+child process before touching torch or a GPU, and exits with its code; under a launcher, a WORLD_SIZE
+that differs from --gpus is an error.
 
 A step renders one full frame: rank r renders rows r, r+N, ... (interleaved tiling) into a
 device buffer and the frame is gathered on rank 0 over RCCL (torch.distributed "nccl" by default, or
@@ -285,19 +289,48 @@ class _Watchdog:
         return False
 
 
+LAUNCH_GUARD = "RTG_BENCH_LAUNCHED"  # set in the ranks bench.py starts itself (no second launch)
+
+
+def self_launch(args):
+    """`--gpus N` (N > 1) without a launcher: start the N ranks here, one process per GPU, as
+    `python -m torch.distributed.run --nproc-per-node N bench.py ...` in a fresh child process, and
+    return its exit code (rank 0's one JSON line goes straight to this process's stdout). Runs before
+    torch is imported or any GPU is touched, and never execs: the driver's plain
+    `bench.py --gpus 8` then measures eight ranks, not one. Returns None when no launch is needed."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    if os.environ.get(LAUNCH_GUARD):
+        sys.exit(f"[bench] --gpus {args.gpus}: a rank started by bench.py has no WORLD_SIZE")
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, **{LAUNCH_GUARD: "1", "MASTER_ADDR": "127.0.0.1"})
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # a launcher with a different rank count: the line would describe another job than asked for
+        sys.exit(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: run with --gpus {world}, or without "
+                 f"a launcher (bench.py starts its own ranks)")
     import numpy as np
     import torch
     import torch.distributed as dist
 
     import rtgpu
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     gloo = args.dist_backend == "gloo"
     if gloo:
         if args.gather_impl == "rtg":

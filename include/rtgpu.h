@@ -312,8 +312,10 @@ rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const r
  * pixels, every k-th row of the shard; counting kernel) counts every node's visits for this camera and the node array
  * is renumbered so the most-visited nodes form that prefix (the "hot treelet"; the root stays first).
  * Traversal order and frames are unchanged: only where a node is read from changes. rtg_render does
- * the same on its first render of a camera; calling this first keeps the probe (~0.2 s for 1M
- * spheres at 4K) out of that render. A no-op for every other schedule and with RTG_TREELET_HOT=0.
+ * the same on the scene's first treelet render only (later cameras keep the tuned order until this is
+ * called for them: a moving camera pays no probe and node re-upload inside its frames); calling this
+ * first keeps the probe (~0.13 s for 1M spheres at 4K) out of that render. A no-op for every other
+ * schedule and with RTG_TREELET_HOT=0.
  * Not concurrent with renders of the same scene (it rewrites the scene's node array). No reference
  * counterpart: the reference's bvh_node keeps its nodes in host memory (bvh_node.hpp:25-77). */
 rtg_status rtg_scene_prepare(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job);

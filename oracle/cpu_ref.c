@@ -728,7 +728,10 @@ static float sin_spec(float x) {
   float z = r * r;
   float sr = fmaf(fmaf(fmaf(-0x1.9943f2p-13f, z, 0x1.11073cp-7f), z, -0x1.555546p-3f) * z, r, r);
   float cr = fmaf(fmaf(fmaf(0x1.99eb9cp-16f, z, -0x1.6c0c34p-10f), z, 0x1.55554ap-5f), z * z, fmaf(-0.5f, z, 1.0f));
-  int q = (int)k & 3;
+  /* quadrant k mod 4 in float, exact for integer-valued k, NaN / inf -> 0: no out-of-range float -> int
+     conversion; accuracy is claimed for |x| < 8192 */
+  float m = k - 4.0f * floorf(0.25f * k);
+  int q = (m >= 0.0f && m < 4.0f) ? (int)m : 0;
   float v = (q & 1) ? cr : sr;
   return (q & 2) ? -v : v;
 }
@@ -899,9 +902,10 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   if (fabsf(q) < 0x1p-100f || a == 0.0f) return -1.0f;
   float t0 = q * inv_a, t1 = c / q; /* far root by the reciprocal, near root divided */
   float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
-  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
-  if (tmin < lo && lo < tmax) return lo;
-  if (tmin < hi && hi < tmax) return hi;
+  /* roots up to tmax inclusive: a root equal to the closest hit is an exact-t tie (tie_wins32) */
+  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
+  if (tmin < lo && lo <= tmax) return lo;
+  if (tmin < hi && hi <= tmax) return hi;
   return -1.0f;
 }
 /* quad::hit, fp32: returns t or -1 */
@@ -921,6 +925,17 @@ static float quad_t32(const float* q, f3 o, f3 d, float tmin, float tmax) {
   return t;
 }
 
+/* Exact-t tie rule of the rtg-f32 spec (rtg_kernels.hip tie_wins): the reference tests
+   its list in order (hittable_list.hpp:40-64), quads accept t == closest (interval::contains,
+   quad.hpp:62), spheres do not (interval::surrounds, sphere.hpp:70). At equal t it keeps any quad over
+   any sphere, the later quad, the earlier sphere, in whatever order they are tested; ids are input
+   (list-order) indices. */
+static int tie_wins32(const world32* w, int64_t id, int64_t best) {
+  int nq = w->s->prims[id].kind == RTG_PRIM_QUAD, bq = w->s->prims[best].kind == RTG_PRIM_QUAD;
+  if (nq != bq) return nq;
+  return nq ? id > best : id < best;
+}
+
 /* closest hit: reference BVH order; boxes tested in f64 (pure culling), primitives in fp32 */
 /* `origin`: the primitive the ray starts on (-1 for camera rays). A quad is planar, so a ray
    leaving it can never hit it again: it is skipped (DESIGN.md §4 "origin rule"). */
@@ -931,7 +946,7 @@ static void node_hit32(const world32* w, int32_t code, f3 o, f3 d, const double 
     float t = w->s->prims[id].kind == RTG_PRIM_SPHERE
                   ? sphere_t32(w->sph + id * 8, o, d, time, 0.001f, *tbest, id == origin)
                   : (id == origin ? -1.0f : quad_t32(w->qd + id * 16, o, d, 0.001f, *tbest));
-    if (t > 0.0f) {
+    if (t > 0.0f && (t < *tbest || tie_wins32(w, id, *best))) {
       *tbest = t;
       *best = id;
     }

@@ -469,6 +469,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   }
   if (out->occluder_prim >= 0) {  // after every referenced sphere, so the refs stay the identity
     const rtg_primitive& p = d->prims[out->occluder_prim];
+    slot[out->occluder_prim] = nsph;
     out->occluder = nsph++;
     const float rec[8] = {static_cast<float>(p.p0[0]),          static_cast<float>(p.p0[1]),
                           static_cast<float>(p.p0[2]),          static_cast<float>(p.radius),
@@ -477,6 +478,11 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->spheres.insert(out->spheres.end(), rec, rec + 8);
   }
 
+  // the exact-t tie rule's list order: input index per sphere slot, then per quad slot
+  out->tie_rank.assign(static_cast<size_t>(nsph) + nquad, -1);
+  for (int64_t i = 0; i < d->num_prims; ++i)
+    if (slot[i] >= 0)
+      out->tie_rank[(d->prims[i].kind == RTG_PRIM_QUAD ? nsph : 0) + slot[i]] = static_cast<int32_t>(i);
   phase("prims");
   // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
   if (out->node_width == 4) {
@@ -828,6 +834,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   }
   const size_t perm_off = total;
   total += (hs.perlin_perm.size() * 4 + 255) & ~size_t(255);
+  const size_t rank_off = total;
+  total += (hs.tie_rank.size() * 4 + 255) & ~size_t(255);
   total = std::max<size_t>(total, 256);
 
   rtg_scene* s = new (std::nothrow) rtg_scene();
@@ -860,6 +868,10 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
       (e = hipMemcpyAsync(base + perm_off, hs.perlin_perm.data(), hs.perlin_perm.size() * 4,
                           hipMemcpyHostToDevice, s->own_stream)) != hipSuccess)
     return cleanup(hip_fail(e, "hipMemcpy(perlin)"));
+  if (!hs.tie_rank.empty() &&
+      (e = hipMemcpyAsync(base + rank_off, hs.tie_rank.data(), hs.tie_rank.size() * 4, hipMemcpyHostToDevice,
+                          s->own_stream)) != hipSuccess)
+    return cleanup(hip_fail(e, "hipMemcpy(tie ranks)"));
   if ((e = hipStreamSynchronize(s->own_stream)) != hipSuccess)
     return cleanup(hip_fail(e, "hipStreamSynchronize(upload)"));
   const auto t2 = std::chrono::steady_clock::now();
@@ -901,6 +913,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.texels = reinterpret_cast<const uint8_t*>(base + parts[7].off);
   s->dev.perlin_vec = reinterpret_cast<const float4*>(base + parts[8].off);
   s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
+  s->dev.tie_rank = reinterpret_cast<const int32_t*>(base + rank_off);
   s->dev.num_nodes = hs.num_nodes;
   s->dev.root_code = 0;
   s->dev.occluder = hs.occluder;
@@ -1124,8 +1137,12 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   // full-frame buffers cost memory. RTG_TILE_SLOTS=0 / >0 forces it off / on.
   const int64_t full_partial_bytes = int64_t(rows) * W * 12 * dj.chunks;
   const bool ring_on = K.tile_slots > 0 || (K.tile_slots < 0 && full_partial_bytes > kRingAutoBytes);
+  // the ring kernels index the frame with 32-bit byte offsets (ring_combine's buffer descriptor: the
+  // shard's frame below 2 GiB) and pack a tile into 25 bits of the per-wave batch table (tile << 7):
+  // larger shards keep the full-frame partials, whose indexing is 64-bit
+  const bool ring_fits = int64_t(rows) * W * 12 < (int64_t(1) << 31) && dj.num_tiles < (1 << 25);
   const bool want_ring = !P->progressive && dj.chunks > 1 && dj.chunks <= (1 << 20) && dc.max_depth > 0 &&
-                         !P->count && ring_on;
+                         !P->count && ring_on && ring_fits;
   dj.ring_log2 = want_ring ? 0 : -1;  // provisional: the LDS layouts reserve the per-wave batch tables
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
@@ -1470,7 +1487,10 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   rtg_status pst = plan_render(s, cam, job, &P);
   if (pst != RTG_OK) return pst;
   const Knobs& K = s->knobs;
-  if (wants_treelet_tune(s, cam, job, P)) {  // first render of this camera: probe, renumber, plan again
+  // the scene's first render on the treelet schedule tunes its hot treelet implicitly (probe, renumber,
+  // plan again); a later camera or shard re-tunes only through rtg_scene_prepare, so a moving camera does
+  // not pay a probe render and a node re-upload inside every frame's rtg_render
+  if (s->treelet_key == 0 && wants_treelet_tune(s, cam, job, P)) {
     pst = rtg_scene_prepare(s, cam, job);
     if (pst != RTG_OK) return pst;
     P = Plan{};

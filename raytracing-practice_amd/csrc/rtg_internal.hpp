@@ -36,6 +36,9 @@ struct HostScene {
   std::vector<uint8_t> texels;
   std::vector<float> perlin_vec;   // 4 floats * 256 per table
   std::vector<int32_t> perlin_perm;  // 3*256 per table
+  // exact-t tie rule: the input (list-order) index of every sphere slot, then of every
+  // quad slot; read by the kernels only when a primitive's root equals the closest hit so far
+  std::vector<int32_t> tie_rank;
   int64_t num_nodes = 0;
   int32_t depth = 0;
   int32_t stack_need = 0;  // traversal stack entries needed (<= depth for BVH2)
@@ -163,6 +166,9 @@ struct DevScene {
   // counting renders of the cache-read schedules: per-node visit counters (node index = code / 112),
   // the probe behind the hot treelet (rtg_api.cpp tune_treelet); null otherwise
   uint32_t* node_visits;
+  // input (reference list-order) index of each sphere slot [0, num_spheres), then of each quad slot
+  // [num_spheres, num_spheres + num_quads): the exact-t tie rule of the rtg-f32 spec
+  const int32_t* tie_rank;
 };
 
 // A render kernel picked for a plan (rtg_kernels.hip choose_kernel); fn == nullptr: none fits.

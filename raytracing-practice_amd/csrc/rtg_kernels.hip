@@ -126,7 +126,12 @@ __device__ __forceinline__ float sin_spec(float x) {
   const float sr = fmaf(fmaf(fmaf(-0x1.9943f2p-13f, z, 0x1.11073cp-7f), z, -0x1.555546p-3f) * z, r, r);
   const float cr = fmaf(fmaf(fmaf(0x1.99eb9cp-16f, z, -0x1.6c0c34p-10f), z, 0x1.55554ap-5f), z * z,
                         fmaf(-0.5f, z, 1.0f));
-  const int q = static_cast<int>(k) & 3;
+  // the quadrant k mod 4 in float (exact for every integer-valued k; NaN / inf fall to 0), so no
+  // float -> int conversion sees an out-of-range value here or in the oracle. The spec's
+  // accuracy claim is |x| < 8192 (three-step reduction); larger arguments stay bit-identical between
+  // kernel and oracle but drift from libm's sin.
+  const float m = k - 4.0f * floorf(0.25f * k);
+  const int q = (m >= 0.0f && m < 4.0f) ? static_cast<int>(m) : 0;
   const float v = (q & 1) ? cr : sr;
   return (q & 2) ? -v : v;
 }
@@ -208,9 +213,11 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
-  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
-  if (tmin < lo && lo < tmax) return lo;
-  if (tmin < hi && hi < tmax) return hi;
+  // roots up to and including tmax: a root equal to the closest hit so far is an exact-t tie, which
+  // the caller resolves by the reference's list order (take_hit)
+  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
+  if (tmin < lo && lo <= tmax) return lo;
+  if (tmin < hi && hi <= tmax) return hi;
   return -1.0f;
 }
 
@@ -232,6 +239,28 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   const float beta = dot(w, cross(u, hp));
   if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return -1.0f;
   return t;
+}
+
+// Exact-t ties (rtg-f32 spec, DESIGN.md §4 "tie rule"). The reference tests the world's objects in
+// list order (hittable_list.hpp:40-64) against a shrinking interval, and its two primitives bound it
+// differently: quad::hit accepts t == closest_so_far (interval::contains, quad.hpp:62, interval.hpp:29),
+// sphere::hit does not (interval::surrounds, sphere.hpp:70, interval.hpp:32). Between primitives at the
+// same t the reference therefore keeps: any quad over any sphere, the later quad in list order, the
+// earlier sphere — whatever order they are tested in. The kernels test in BVH order, so both primitive
+// tests return roots up to tmax inclusive and a root equal to the closest hit wins only by that rule
+// (S.tie_rank: each slot's list index, read only on a tie). Not a root at t == tbest: th < tbest.
+__device__ __forceinline__ bool tie_wins(const DevScene& S, int32_t ref, int32_t best) {
+  const bool nq = (ref & kQuadRefBit) != 0, bq = (best & kQuadRefBit) != 0;
+  if (nq != bq) return nq;
+  const int64_t off = nq ? S.num_spheres : 0;
+  const int32_t rn = S.tie_rank[off + (ref & ~kQuadRefBit)], rb = S.tie_rank[off + (best & ~kQuadRefBit)];
+  return nq ? rn > rb : rn < rb;
+}
+// A primitive test's root th (-1: miss; else tmin < th <= tbest) replaces the closest hit.
+__device__ __forceinline__ bool take_hit(const DevScene& S, float th, float tbest, int32_t ref, int32_t best) {
+  if (!(th > 0.0f)) return false;
+  if (__builtin_expect(th < tbest, 1)) return true;
+  return tie_wins(S, ref, best);
 }
 
 template <bool COUNT>
@@ -557,7 +586,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
-      if (th > 0.0f) {
+      if (take_hit(S, th, t.tbest, first + k, t.best)) {
         t.tbest = th;
         t.best = first + k;
         if (MAT) t.mat = ibits(sp4[1].w);
@@ -580,7 +609,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
     }
-    if (th > 0.0f) {  // th > tmin >= 0.001 on a hit
+    if (take_hit(S, th, t.tbest, ref, t.best)) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
       t.best = ref;
       if (MAT) t.mat = m;
@@ -678,7 +707,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
           const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
           t = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
         }
-        if (t > 0.0f) {  // t > tmin >= 0.001 on a hit
+        if (take_hit(S, t, tbest, ref, best)) {  // t > tmin >= 0.001 on a hit
           tbest = t;
           best = ref;
         }

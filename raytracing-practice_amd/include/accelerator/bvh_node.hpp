@@ -36,16 +36,19 @@ class bvh_node : public hittable {
     std::call_once(once_, [this]() {
       if (built_) return;
       std::vector<std::shared_ptr<hittable>> objects(list_order);
-      const_cast<bvh_node*>(this)->build(objects, 0, objects.size());
+      // the root's box was set in the constructor (the same union): not rewritten here, where other
+      // threads may already read it through bounding_box()
+      const_cast<bvh_node*>(this)->build(objects, 0, objects.size(), false);
       built_ = true;
     });
   }
 
-  void build(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end) {
+  void build(std::vector<std::shared_ptr<hittable>>& objects, size_t start, size_t end, bool set_box = true) {
     if (start >= end) return;  // an empty list: no children, every ray misses the empty box
-    bbox = aabb::empty;
-    for (size_t i = start; i < end; ++i) bbox = aabb(bbox, objects[i]->bounding_box());
-    const int axis = bbox.longest_axis();
+    aabb box = aabb::empty;
+    for (size_t i = start; i < end; ++i) box = aabb(box, objects[i]->bounding_box());
+    if (set_box) bbox = box;
+    const int axis = box.longest_axis();
     const size_t span = end - start;
     if (span == 1) {
       left = right = objects[start];
@@ -80,6 +83,7 @@ class bvh_node : public hittable {
         if (!obj->rtg_flatten(sb, offset)) return false;
       return true;
     }
+    if (!left) return true;  // built over an empty list: nothing to flatten
     if (!left->rtg_flatten(sb, offset)) return false;
     return right == left || right->rtg_flatten(sb, offset);
   }

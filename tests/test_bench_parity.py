@@ -35,3 +35,53 @@ def test_cpu_parity_against_the_oracle(scenes, oracle):
     # a uniformly shifted frame fails the tolerance
     off = bench.cpu_parity(s.desc, cam, rows + np.float32(0.01), first, step, seed, threads=2)
     assert not off["pass"]
+
+
+def _args(gpus):
+    import types
+    return types.SimpleNamespace(gpus=gpus)
+
+
+def test_self_launch_starts_n_ranks(monkeypatch):
+    """`bench.py --gpus N` without a launcher starts torch.distributed.run with N ranks as a child
+    process (never an exec) and returns its exit code; one GPU or an existing launcher: no launch."""
+    import subprocess
+    import sys
+
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, env=None, **kw):
+        seen["cmd"], seen["env"] = cmd, env
+        return Done()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv(bench.LAUNCH_GUARD, raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--steps", "3"])
+    assert bench.self_launch(_args(8)) == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "8", "--steps", "3"] and cmd[-5].endswith("bench.py")
+    assert seen["env"][bench.LAUNCH_GUARD] == "1"
+    seen.clear()
+    assert bench.self_launch(_args(1)) is None and not seen
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    assert bench.self_launch(_args(8)) is None and not seen
+
+
+def test_world_size_mismatch_exits_nonzero():
+    """Under a launcher whose WORLD_SIZE differs from --gpus the line would describe another job:
+    bench.py exits non-zero before touching torch or a GPU."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, bench.__file__, "--gpus", "8"], env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

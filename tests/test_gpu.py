@@ -283,15 +283,25 @@ def test_hot_treelet_keeps_the_frame(gpu_lib, scenes, oracle, monkeypatch):
     assert 500 < p1.treelet_visit_permille <= 1000, p1.as_dict()  # the LDS prefix takes most visits
     hot, hst = ds.render_host(c)
     assert np.array_equal(hot, bfs) and hst.segments == bst.segments
-    # another camera (here: other rows) is not the tuned one until its first render re-tunes
+    # another camera is not the tuned one; its renders keep the tuned order (no probe inside
+    # rtg_render after the scene's first tuning) until rtg_scene_prepare re-tunes
     c2 = rtgpu.rtg_camera_desc.from_buffer_copy(c)
     c2.lookfrom[0] += 3.0
     assert ds.plan(c2).treelet_hot == 0
     hot2, st2 = ds.render_host(c2)
+    assert ds.plan(c2).treelet_hot == 0 and ds.plan(c).treelet_hot == 1
+    ds.prepare(c2)
     assert ds.plan(c2).treelet_hot == 1 and ds.plan(c).treelet_hot == 0
+    hot3, st3 = ds.render_host(c2)
+    assert np.array_equal(hot3, hot2) and st3.segments == st2.segments
     ds.close()
     o, segs = oracle.render_f32(s.desc, c2)
     assert_parity(hot2, o, st2, segs)
+    # a fresh scene's first render tunes implicitly
+    ds = gpu_lib.scene_create(s.desc)
+    ds.render_host(c2)
+    assert ds.plan(c2).treelet_hot == 1
+    ds.close()
     b = scenes.build("bouncing_spheres", grid=11, rand_seed=1)
     cb = rtgpu.rtg_camera_desc.from_buffer_copy(b.camera)
     cb.image_width, cb.samples_per_pixel = 96, 4
@@ -404,6 +414,60 @@ def test_tile_ring_matches_full_frame_partials(gpu_lib, scenes, name, W, spp, sc
     assert float(ref.sum()) > 0.0
     for slots, (frame, segs) in out.items():
         assert np.array_equal(frame, ref) and segs == ref_segs, slots
+
+
+@pytest.mark.parametrize("schedule", [3, 5])
+@pytest.mark.parametrize("world", [3, 8])
+def test_tile_ring_on_strided_shards(gpu_lib, scenes, schedule, world, monkeypatch):
+    """The ring's tile -> pixel mapping for row-interleaved shards (row_stride > 1: 16x4 tiles,
+    tile_lw 4 — the layout of multi-rank renders): every rank's shard through rings of 1
+    and 8 slots equals the same shard through the full-frame partials, pixel for pixel and segment for
+    segment."""
+    import ctypes as C
+
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 136, 40, 30
+    H = gpu_lib.camera_resolve(c).image_height
+    W = c.image_width
+    for r in range(world):
+        b, stride, n = rtgpu.shard_rows(H, r, world)
+        out = {}
+        for slots in ("0", "1", "8"):
+            monkeypatch.setenv("RTG_TILE_SLOTS", slots)
+            ds = gpu_lib.scene_create(s.desc)
+            p = ds.plan(c, row_begin=b, row_stride=stride, row_count=n)
+            assert p.tile_slots == int(slots), p.as_dict()
+            frame = np.zeros((n, W, 3), dtype=np.float32)
+            st = rtgpu.rtg_render_stats()
+            job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, b, stride, n, rtgpu.RTG_RENDER_SCHEDULE(schedule), None)
+            gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job),
+                                                                frame.ctypes.data, C.byref(st)))
+            ds.close()
+            out[slots] = (frame, st.segments)
+        ref, ref_segs = out.pop("0")
+        assert float(ref.sum()) > 0.0
+        for slots, (frame, segs) in out.items():
+            assert np.array_equal(frame, ref) and segs == ref_segs, (r, slots)
+
+
+def test_tile_ring_bounds_fall_back_to_full_frame(gpu_lib, scenes):
+    """The ring kernels index the shard's frame with 32-bit byte offsets: a shard of >= 2 GiB (here
+    18432 x 10368 px x 12 B) keeps the full-frame partials even where the ring would be the default
+    (above 4 GiB of partials); just below the bound the ring is chosen (plans only, nothing rendered)."""
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.samples_per_pixel, c.max_depth = 1000, 50
+    ds = gpu_lib.scene_create(s.desc)
+    c.image_width = 18432
+    H = gpu_lib.camera_resolve(c).image_height
+    p = ds.plan(c)
+    assert H * 18432 * 12 >= 1 << 31 and p.tile_slots == 0 and p.partial_bytes == H * 18432 * 12 * p.chunks
+    c.image_width = 12288  # 12288 x 6912 x 12 B < 2 GiB
+    H = gpu_lib.camera_resolve(c).image_height
+    p = ds.plan(c)
+    assert H * 12288 * 12 < 1 << 31 and p.tile_slots > 0, p.as_dict()
+    ds.close()
 
 
 def test_progressive_chunks_and_checkpoint(gpu_lib, scenes):
@@ -533,6 +597,24 @@ def test_ground_and_one_sphere(gpu_lib, oracle, bvh):
         finally:
             del os.environ["RTG_NO_OCCLUDER"]
         assert np.array_equal(g, g2) and st2.segments == st.segments
+
+
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
+def test_exact_t_ties_match_oracle(gpu_lib, oracle, bvh):
+    """The exact-t tie rule: identical quads and identical spheres
+    hit at bit-identical t. Whatever order a BVH builder makes the kernel test them in, the frame is
+    cpu_ref32's bit for bit, showing the later quad (interval::contains, quad.hpp:62) and the earlier
+    sphere (interval::surrounds, sphere.hpp:70), as the reference's list order keeps them."""
+    from tie_scene import BLUE, GREEN, RED, WHITE, colour_counts, tie_scene
+
+    d, cam = tie_scene(bvh, width=96)
+    ds = gpu_lib.scene_create(d)
+    g, st = ds.render_host(cam)
+    ds.close()
+    o, segs = oracle.render_f32(d, cam)
+    assert np.array_equal(g, o) and st.segments == segs
+    n = colour_counts(g)
+    assert n[GREEN] > 200 and n[BLUE] > 100 and n[RED] == 0 and n[WHITE] == 0, n
 
 
 def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypatch):
@@ -919,6 +1001,28 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     assert line["parity"]["identical_frac"] > 0.999
     assert all(g is not None and g >= 0 for g in line["gather_ms"])
     assert line["cpu_baseline"] is None  # rank 0 at N = 1 only
+
+
+def test_bench_launches_its_own_ranks(tmp_path):
+    """A plain `bench.py --gpus 2` (no torch.distributed.run around it, as a driver may invoke
+    `bench.py --gpus 8`) starts its two ranks itself: the line must say n_gpus 2,
+    carry both ranks' records and pass the per-pixel check of the gathered frame. gloo: two ranks share
+    this one GPU (RCCL takes one rank per device)."""
+    import json
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--width", "160", "--height", "90", "--spp", "4", "--depth", "8", "--steps", "1", "--warmup", "1",
+           "--parity-seconds", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=str(tmp_path), env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and [x["rank"] for x in line["ranks"]] == [0, 1]
+    assert [x["rows"] for x in line["ranks"]] == [45, 45]
+    assert line["parity"]["pass"] and line["parity"]["identical_frac"] > 0.999, line["parity"]
 
 
 def test_numerics_helpers_match_ieee():

@@ -109,6 +109,11 @@ def test_texture_transcendentals_are_accurate(oracle):
     e3 = max(abs(oracle.acos_spec(float(y)) - math.acos(float(y))) for y in v[:, 1])
     assert e3 < 5e-7, e3
     assert oracle.acos_spec(1.0) == 0.0 and oracle.acos_spec(-1.0) == np.float32(np.pi)
+    # outside the claimed range the quadrant is still well defined (k mod 4 in float, no out-of-range
+    # float -> int conversion): NaN for NaN / inf, and negative quadrants keep sin's symmetry
+    assert all(math.isnan(oracle.sin_spec(x)) for x in (float("nan"), float("inf"), float("-inf")))
+    for x in (0.3, 2.0, 4.0, 5.5, 100.25):
+        assert oracle.sin_spec(-x) == -oracle.sin_spec(x)
 
 
 def test_direct_sampling_is_accurate_and_uniform(oracle):
@@ -197,3 +202,18 @@ def test_sphere_t32_grazing_far_spheres(oracle):
     assert checked > 2000
     assert bad_new == 0, (bad_new, checked)
     assert bad_old > 0.3 * checked, (bad_old, checked)
+
+
+def test_exact_t_ties_follow_reference_list_order(oracle):
+    """Exact-t tie rule of the rtg-f32 spec: identical quads and identical spheres hit at
+    bit-identical t. The reference keeps the later quad (interval::contains, quad.hpp:62) and the
+    earlier sphere (interval::surrounds, sphere.hpp:70) — cpu_ref32 must do the same whatever order
+    its BVH tests them in."""
+    from tie_scene import BLUE, GREEN, RED, WHITE, colour_counts, tie_scene
+
+    for bvh in (rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_MEDIAN):
+        d, cam = tie_scene(bvh)
+        frame, _ = oracle.render_f32(d, cam)
+        n = colour_counts(frame)
+        assert n[GREEN] > 50 and n[BLUE] > 30, n  # the later quad, the earlier sphere
+        assert n[RED] == 0 and n[WHITE] == 0, n

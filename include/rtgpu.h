@@ -300,7 +300,11 @@ typedef struct rtg_launch_plan {
   int32_t treelet_tune_us;   /* host + probe time of the scene's last hot-treelet tuning */
   int32_t treelet_visit_permille; /* treelet_hot: of the probe's node visits, the share (per mille)
                                      that the treelet_nodes in LDS take */
-  int32_t reserved_[3];
+  /* round 4, layout-compatible (two of ABI 5's reserved words): */
+  int32_t ray_queue;         /* > 0: rays move between the waves of a workgroup through LDS queues (the
+                                RTG_RAY_QUEUE prototype; the shade queue's capacity), 0: off */
+  int32_t node_width;        /* BVH node width the kernels traverse: 2, 4, or 8 (RTG_BVH_WIDTH=8 A/B) */
+  int32_t reserved_[1];
 } rtg_launch_plan;
 
 rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,

@@ -51,7 +51,7 @@ constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
 constexpr int64_t kRingAutoBytes = int64_t(4) << 30;  // full-frame partials above this: the tile ring
-constexpr int kNumCounters = 26;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring)
+constexpr int kNumCounters = 28;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring, [26] ray queues)
 // gfx950 allocates a workgroup's LDS in 1280-byte granules (160 KB = 128 of them): measured with the
 // dual launch, whose two workgroups stop sharing a CU exactly when the rounded sizes pass 160 KB
 constexpr int kLdsGranule = 1280;
@@ -235,6 +235,8 @@ Knobs read_knobs() {
   if (num("RTG_TILE_SLOTS", 0, 65536, &ts) && (ts & (ts - 1)) == 0) k.tile_slots = ts;
   num("RTG_TREELET_STACK", 4, 16, &k.treelet_stack);
   num("RTG_TREELET_HOT", 0, 1, &k.treelet_hot);
+  num("RTG_RAY_QUEUE", 0, 1, &k.ray_queue);
+  num("RTG_Q_DEPOSIT", 1, 64, &k.q_deposit);
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -272,6 +274,63 @@ void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
   put(o->w, w);
   put(o->defocus_disk_u, defocus_radius * u);
   put(o->defocus_disk_v, defocus_radius * v);
+}
+
+// W-wide nodes, 28 W bytes: lo.x[W], lo.y[W], lo.z[W], hi.x[W], hi.y[W], hi.z[W], code[W]; inner child
+// codes are byte offsets of the child node, leaf codes ~((first << 3) | (count - 1)), empty slots
+// kEmptyChild with the inverted box (+inf, -inf). Boxes rounded outward to fp32.
+template <int W>
+bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
+  constexpr int64_t kBytes = node_bytes(W), kWords = 7 * W;
+  if (t.nodes.size() > static_cast<size_t>(INT32_MAX / kBytes)) {
+    *err = "BVH too large for 32-bit node offsets";
+    return false;
+  }
+  out->nodes.resize(t.nodes.size() * kWords);
+  const int64_t nn = static_cast<int64_t>(t.nodes.size());
+  std::vector<int> bad(host_threads(nn), 0);  // 1: a node without children, 2: a leaf not encodable
+  host_par_for(nn, [&](int64_t b, int64_t e, int th) {
+    for (int64_t k = b; k < e && !bad[th]; ++k) {
+      const BuildNodeW<W>& n = t.nodes[k];
+      float* f = &out->nodes[k * kWords];
+      if (n.child[0] == kEmptyChild) {
+        bad[th] = 1;
+        break;
+      }
+      for (int c = 0; c < W; ++c) {
+        int32_t code = kEmptyChild;
+        const bool empty = n.child[c] == kEmptyChild;
+        if (!empty) {
+          if (n.child[c] >= 0) {
+            code = static_cast<int32_t>(n.child[c] * kBytes);  // inner children: byte offset of the node
+          } else {
+            const int64_t first = -(static_cast<int64_t>(n.child[c]) + 1);
+            if (n.count[c] < 1 || n.count[c] > 8 || first >= (int64_t(1) << 28)) {
+              bad[th] = 2;
+              break;
+            }
+            code = ~static_cast<int32_t>((first << 3) | (n.count[c] - 1));
+          }
+        }
+        for (int a = 0; a < 3; ++a) {
+          f[a * W + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
+          f[3 * W + a * W + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
+        }
+        f[6 * W + c] = ibits_to_float(code);
+      }
+    }
+  });
+  for (const int b : bad) {
+    if (b == 1) {
+      *err = "wide BVH node without children";
+      return false;
+    }
+    if (b == 2) {
+      *err = "BVH leaf not encodable";
+      return false;
+    }
+  }
+  return true;
 }
 
 bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
@@ -387,6 +446,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   out->stack_need = bvh.depth;
   out->node_width = 2;
   Bvh4 bvh4;
+  Bvh8 bvh8;
   if (gpu_bvh) {
     out->gpu_bvh = true;
     out->node_width = 4;
@@ -411,14 +471,34 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         cp.max_leaf = std::min(8, std::max(1, ml));
       }
     }
-    collapse_bvh4(bvh, &bvh4, cp);
-    phase("collapse");
-    reorder_top_bfs(&bvh4, kTreeletBfsNodes);
-    phase("bfs");
-    out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
-    out->depth = bvh4.depth;
-    out->stack_need = bvh4.max_pushes;
-    out->node_width = 4;
+    // RTG_BVH_WIDTH=8 (A/B): 8-wide nodes for the cache-read schedules, traversed with
+    // one stack entry per node (the node and its hit children not yet visited), so the stack holds at
+    // most one entry per tree level
+    const char* wenv = std::getenv("RTG_BVH_WIDTH");
+    if (wenv && std::atoi(wenv) == 8) {
+      collapse_bvh<8>(bvh, &bvh8, cp);
+      phase("collapse");
+      // a stack entry packs the node's byte offset / 32 into 24 bits beside the 8-bit child mask
+      if (static_cast<int64_t>(bvh8.nodes.size()) * node_bytes(8) >= (int64_t(1) << 29)) {
+        *err = "8-wide BVH too large for its stack entries (RTG_BVH_WIDTH=8)";
+        return false;
+      }
+      reorder_top_bfs(&bvh8, kTreeletBfsNodes);
+      phase("bfs");
+      out->num_nodes = static_cast<int64_t>(bvh8.nodes.size());
+      out->depth = bvh8.depth;
+      out->stack_need = bvh8.depth;
+      out->node_width = 8;
+    } else {
+      collapse_bvh4(bvh, &bvh4, cp);
+      phase("collapse");
+      reorder_top_bfs(&bvh4, kTreeletBfsNodes);
+      phase("bfs");
+      out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
+      out->depth = bvh4.depth;
+      out->stack_need = bvh4.max_pushes;
+      out->node_width = 4;
+    }
   }
   if (std::getenv("RTG_VERBOSE"))
     std::fprintf(stderr, "[rtg] bvh: %lld primitives, %zu binary nodes -> %lld nodes of width %d, depth %d, stack %d\n",
@@ -485,57 +565,8 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       out->tie_rank[(d->prims[i].kind == RTG_PRIM_QUAD ? nsph : 0) + slot[i]] = static_cast<int32_t>(i);
   phase("prims");
   // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
-  if (out->node_width == 4) {
-    // 4-wide nodes, 112 B: lo.x[4], lo.y[4], lo.z[4], hi.x[4], hi.y[4], hi.z[4], code[4]
-    if (bvh4.nodes.size() > static_cast<size_t>(INT32_MAX / 112)) {
-      *err = "BVH too large for 32-bit node offsets";
-      return false;
-    }
-    out->nodes.resize(bvh4.nodes.size() * 28);
-    const int64_t nn = static_cast<int64_t>(bvh4.nodes.size());
-    std::vector<int> bad(host_threads(nn), 0);  // 1: a node without children, 2: a leaf not encodable
-    host_par_for(nn, [&](int64_t b, int64_t e, int t) {
-      for (int64_t k = b; k < e && !bad[t]; ++k) {
-        const BuildNode4& n = bvh4.nodes[k];
-        float* f = &out->nodes[k * 28];
-        if (n.child[0] == kEmptyChild) {
-          bad[t] = 1;
-          break;
-        }
-        for (int c = 0; c < 4; ++c) {
-          int32_t code = kEmptyChild;
-          const bool empty = n.child[c] == kEmptyChild;
-          if (!empty) {
-            if (n.child[c] >= 0) {
-              code = n.child[c] * 112;  // inner children: byte offset of the node
-            } else {
-              const int64_t first = -(static_cast<int64_t>(n.child[c]) + 1);
-              if (n.count[c] < 1 || n.count[c] > 8 || first >= (int64_t(1) << 28)) {
-                bad[t] = 2;
-                break;
-              }
-              code = ~static_cast<int32_t>((first << 3) | (n.count[c] - 1));
-            }
-          }
-          for (int a = 0; a < 3; ++a) {
-            f[a * 4 + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
-            f[12 + a * 4 + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
-          }
-          f[24 + c] = ibits_to_float(code);
-        }
-      }
-    });
-    for (const int b : bad) {
-      if (b == 1) {
-        *err = "4-wide BVH node without children";
-        return false;
-      }
-      if (b == 2) {
-        *err = "BVH leaf not encodable";
-        return false;
-      }
-    }
-  }
+  if (out->node_width == 4 && !emit_wide(bvh4, out, err)) return false;
+  if (out->node_width == 8 && !emit_wide(bvh8, out, err)) return false;
   // child-pair nodes: 64 B
   if (out->node_width == 2) out->nodes.resize(bvh.nodes.size() * 16);
   for (size_t k = 0; out->node_width == 2 && k < bvh.nodes.size(); ++k) {
@@ -920,7 +951,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.sphere_f4 = 2;
   s->dev.treelet_bytes = 0;  // set per render by the treelet schedule
   s->dev.treelet_lds = 0;
-  s->dev.node_limit = static_cast<int32_t>(std::min<int64_t>(hs.num_nodes * 112, INT32_MAX));
+  s->dev.node_limit = static_cast<int32_t>(
+      std::min<int64_t>(hs.num_nodes * node_bytes(hs.node_width == 8 ? 8 : 4), INT32_MAX));
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
   s->dev.num_quads = static_cast<int64_t>(hs.quads.size() / 20);
@@ -1011,6 +1043,8 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
   if (c[24] != 0)
     return fail(RTG_E_HIP, "tile-ring slot waits timed out (frame incomplete) in " + std::to_string(c[24]) + " waves");
+  if (c[26] != 0)
+    return fail(RTG_E_HIP, "ray-queue waits timed out (frame incomplete) in " + std::to_string(c[26]) + " waves");
   if (c[7] != 0)
     return fail(RTG_E_UNSUPPORTED, "the 16-bit LDS stack layout cannot hold this tree's codes in " +
                                        std::to_string(c[7]) + " workgroups (nothing rendered)");
@@ -1087,6 +1121,7 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
 
   DevJob& dj = P->dj;
   dj = DevJob{};
+  dj.lds_queue = -1;
   dj.seed_mix = mix64(job->seed);
   dj.row_begin = job->row_begin;
   dj.row_stride = job->row_stride;
@@ -1205,9 +1240,9 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   }
   // default: the whole scene in LDS (3); else the top of a 4-wide tree in LDS (5, config 5's 1M
   // spheres: -1.3 % against 4, profiles/r02_ab), else the plain grid (4)
-  if (variant == 0) variant = lds_bytes > 0 ? 3 : (dscene.node_width == 4 ? 5 : 4);
-  if (variant == 5) {  // persistent workgroups with the top of the tree in LDS (4-wide trees)
-    if (dscene.node_width != 4) return fail(RTG_E_INVALID, "schedule 5 needs a 4-wide BVH (RTG_BVH_SAH)");
+  if (variant == 0) variant = lds_bytes > 0 ? 3 : (dscene.node_width >= 4 ? 5 : 4);
+  if (variant == 5) {  // persistent workgroups with the top of the tree in LDS (4- or 8-wide trees)
+    if (dscene.node_width < 4) return fail(RTG_E_INVALID, "schedule 5 needs a wide BVH (RTG_BVH_SAH)");
     dj.stack_esz = 4;
     dj.lds_waves = kLdsWaves;
     // LDS stack entries: trees that spill anyway may keep fewer of them in LDS and more treelet nodes
@@ -1286,6 +1321,26 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     j4.lds_ring = l4[9];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
+  // ray queues (RTG_RAY_QUEUE prototype): the small-scene schedule (five 4-wave
+  // workgroups per CU, 16-bit stacks, no image / noise textures) of one-shot frames without the tile
+  // ring; the queues go after the scene copy, as large as five workgroups per CU still allow
+  if (K.ray_queue && variant == 3 && dj.lds_waves == 4 && lds_wgs == kSmallSceneWgs && lds4 < 0 &&
+      dj.stack_esz == 2 && !dscene.tex_full && dj.ring_log2 < 0 && !P->skip_kernel) {
+    const int qoff = (lds_bytes + 15) & ~15;
+    for (const int T : {128, 64, 32}) {
+      const int Sq = 64;
+      const int qbytes = (kQCtl + kQShadeFields * Sq + kQTraceFields * T) * 4;
+      if (lds_alloc(qoff + qbytes) * kSmallSceneWgs <= kLdsPerCu) {
+        dj.lds_queue = qoff;
+        dj.q_shade = Sq;
+        dj.q_trace = T;
+        dj.q_rmax = kQTracerWaves * 64 + Sq + T;  // no queue deadlock below this (rtg_kernels.hip)
+        dj.q_deposit = K.q_deposit;
+        lds_bytes = qoff + qbytes;
+        break;
+      }
+    }
+  }
   P->j4 = j4;
   P->variant = variant;
   P->lds_bytes = lds_bytes;
@@ -1320,7 +1375,7 @@ uint64_t treelet_key(const rtg_camera_desc* c, const rtg_render_desc* j) {
 }
 
 bool wants_treelet_tune(const rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, const Plan& P) {
-  return P.variant == 5 && !P.count && s->knobs.treelet_hot && s->dev.node_width == 4 &&
+  return P.variant == 5 && !P.count && s->knobs.treelet_hot && s->dev.node_width >= 4 &&
          treelet_key(cam, job) != s->treelet_key;
 }
 
@@ -1370,11 +1425,13 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   }
   std::vector<uint32_t> cnt;
   std::vector<int32_t> rec;
+  const int width = s->dev.node_width;
+  const int64_t nb = node_bytes(width);
   if (st == RTG_OK) {
     cnt.resize(n);
-    rec.resize(n * 28);
+    rec.resize(n * nb / 4);
     e = hipMemcpyAsync(cnt.data(), visits, n * 4, hipMemcpyDeviceToHost, os);
-    if (e == hipSuccess) e = hipMemcpyAsync(rec.data(), s->dev.nodes, n * 112, hipMemcpyDeviceToHost, os);
+    if (e == hipSuccess) e = hipMemcpyAsync(rec.data(), s->dev.nodes, n * nb, hipMemcpyDeviceToHost, os);
     if (e == hipSuccess) e = hipStreamSynchronize(os);
     if (e != hipSuccess) st = hip_fail(e, "hot treelet download");
   }
@@ -1382,8 +1439,8 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   (void)hipFree(visits);
   if (st != RTG_OK) return st;
   std::vector<int32_t> order;
-  hot_order_nodes4(rec.data(), cnt.data(), n, &order);
-  e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), rec.data(), n * 112, hipMemcpyHostToDevice, os);
+  hot_order_nodes(rec.data(), width, cnt.data(), n, &order);
+  e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), rec.data(), n * nb, hipMemcpyHostToDevice, os);
   if (e == hipSuccess) e = hipStreamSynchronize(os);
   if (e != hipSuccess) return hip_fail(e, "hot treelet upload");
   s->treelet_tune_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1430,7 +1487,7 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
   out->stack_entry_bytes = P.dj.stack_esz;
   out->lds_stack_entries = P.dj.lds_stack;
   out->spill_entries = P.dj.spill_depth;
-  out->treelet_nodes = P.variant == 5 ? P.dscene.treelet_bytes / 112 : 0;
+  out->treelet_nodes = P.variant == 5 ? P.dscene.treelet_bytes / node_bytes(P.dscene.node_width) : 0;
   out->shade_batch = P.dj.shade_batch;
   out->leaf_batch = P.dj.leaf_batch;
   out->chunk_samples = P.dj.chunk_samples;
@@ -1439,10 +1496,12 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
                                                      : static_cast<int64_t>(P.out_bytes) * P.dj.chunks;
   out->tile_slots = P.ring_slots;
   out->num_cus = s->num_cus;
+  out->ray_queue = P.dj.lds_queue >= 0 ? P.dj.q_shade : 0;
+  out->node_width = P.dscene.node_width;
   if (P.variant == 5) {
     out->treelet_hot = s->treelet_key == treelet_key(cam, job) ? 1 : 0;
     out->treelet_tune_us = static_cast<int32_t>(std::min(s->treelet_tune_ms * 1e3, 2e9));
-    const int64_t tn = P.dscene.treelet_bytes / 112;
+    const int64_t tn = P.dscene.treelet_bytes / node_bytes(P.dscene.node_width);
     if (out->treelet_hot && !s->treelet_cum.empty() && s->treelet_cum.back() > 0)
       out->treelet_visit_permille = static_cast<int32_t>(
           1000 * s->treelet_cum[std::min<int64_t>(tn, static_cast<int64_t>(s->treelet_cum.size()) - 1)] /

@@ -532,20 +532,22 @@ void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]) {
   }
 }
 
-// SAH-optimal 4-wide collapse (the dynamic program of Ylitie, Karras and Laine, "Efficient
-// Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs", HPG 2017, for width 4): for every
-// binary subtree and every budget i = 1..4 of slots it may occupy under a wide parent, the cheapest
+// SAH-optimal W-wide collapse (the dynamic program of Ylitie, Karras and Laine, "Efficient
+// Incoherent Ray Traversal on GPUs Through Compressed Wide BVHs", HPG 2017, at width W = 4 or 8): for
+// every binary subtree and every budget i = 1..W of slots it may occupy under a wide parent, the cheapest
 // representation by surface-area cost — one slot that is a merged leaf (its primitives are a
 // contiguous ref range, <= max_leaf of them) or a wide node, or its two children sharing the budget.
 // cost(wide node) = area x c_node + its slots; cost(leaf) = area x count x 1.
+namespace {
+template <int W>
 struct CollapseDp {
   const Bvh& bin;
   double c_node;
   int max_leaf;
-  std::vector<double> cost;   // [node][i], i = 0..3 for budgets 1..4
+  std::vector<double> cost;   // [node][i], i = 0..W-1 for budgets 1..W
   std::vector<int8_t> pick;   // [node][i]: -1 = budget i-1 (i > 0), 0 = one slot, k = k slots to the left child
   std::vector<uint8_t> as_leaf;  // budget 1: merged leaf (1) or wide node (0)
-  std::vector<int8_t> wide_k;    // slots of the left child when the node is a wide node (d[4])
+  std::vector<int8_t> wide_k;    // slots of the left child when the node is a wide node (d[W])
   std::vector<int64_t> first, count;
   std::vector<Box> box;
 
@@ -564,15 +566,15 @@ struct CollapseDp {
     }
     return s;
   }
-  double slot_cost(const SlotRef& s, int i) const {  // budget i (1..4)
+  double slot_cost(const SlotRef& s, int i) const {  // budget i (1..W)
     if (s.code < 0) return half_area(s.b) * s.cnt;
-    return cost[static_cast<size_t>(s.code) * 4 + (i - 1)];
+    return cost[static_cast<size_t>(s.code) * W + (i - 1)];
   }
 
   void run() {
     const size_t n = bin.nodes.size();
-    cost.assign(n * 4, 0.0);
-    pick.assign(n * 4, 0);
+    cost.assign(n * W, 0.0);
+    pick.assign(n * W, 0);
     as_leaf.assign(n, 0);
     wide_k.assign(n, 0);
     first.assign(n, 0);
@@ -605,9 +607,9 @@ struct CollapseDp {
       const bool two = nd.child[1] != kEmptyChild;
       const SlotRef l = slot_of(m, 0);
       const SlotRef r = two ? slot_of(m, 1) : SlotRef{};
-      double d[5];  // d[j]: the two children sharing j slots
-      int dk[5];
-      for (int j = 1; j <= 4; ++j) {
+      double d[W + 1];  // d[j]: the two children sharing j slots
+      int dk[W + 1];
+      for (int j = 1; j <= W; ++j) {
         d[j] = kInf;
         dk[j] = 0;
         if (!two) {  // a single child: it takes the whole budget
@@ -625,13 +627,13 @@ struct CollapseDp {
       }
       const double a = half_area(box[m]);
       const double c_leaf = c <= max_leaf ? a * static_cast<double>(c) : kInf;
-      const double c_int = a * c_node + d[4];
-      double* cm = &cost[static_cast<size_t>(m) * 4];
-      int8_t* pm = &pick[static_cast<size_t>(m) * 4];
+      const double c_int = a * c_node + d[W];
+      double* cm = &cost[static_cast<size_t>(m) * W];
+      int8_t* pm = &pick[static_cast<size_t>(m) * W];
       as_leaf[m] = c_leaf <= c_int;
       cm[0] = std::min(c_leaf, c_int);
       pm[0] = 0;
-      for (int i = 2; i <= 4; ++i) {
+      for (int i = 2; i <= W; ++i) {
         if (d[i] < cm[i - 2]) {
           cm[i - 1] = d[i];
           pm[i - 1] = static_cast<int8_t>(dk[i]);
@@ -640,17 +642,20 @@ struct CollapseDp {
           pm[i - 1] = -1;
         }
       }
-      wide_k[m] = static_cast<int8_t>(dk[4]);  // m as a wide node: its children share four slots so
+      wide_k[m] = static_cast<int8_t>(dk[W]);  // m as a wide node: its children share W slots so
     }
   }
 };
 
-void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
+}  // namespace
+
+template <int W>
+void collapse_bvh(const Bvh& bin, BvhW<W>* out, const CollapseParams& prm) {
   out->nodes.clear();
   out->depth = 0;
   out->max_pushes = 0;
   if (bin.nodes.empty()) return;
-  CollapseDp dp{bin, prm.c_node, prm.max_leaf, {}, {}, {}, {}, {}, {}, {}};
+  CollapseDp<W> dp{bin, prm.c_node, prm.max_leaf, {}, {}, {}, {}, {}, {}, {}};
   if (prm.sah) dp.run();
   struct Slot {
     int32_t code, count;
@@ -669,20 +674,20 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
   // recursive collapse into pre-allocated nodes; tracks depth and stack pushes on the path
   struct Rec {
     const Bvh& bin;
-    Bvh4* out;
+    BvhW<W>* out;
     decltype(slot_of)& slot;
-    const CollapseDp* dp;  // SAH-optimal collapse, or null: greedy (open the largest-area inner child)
-    // up to four slots, no heap (the collapse visits every node of a 1M-primitive tree)
+    const CollapseDp<W>* dp;  // SAH-optimal collapse, or null: greedy (open the largest-area inner child)
+    // up to W slots, no heap (the collapse visits every node of a 1M-primitive tree)
     struct Slots {
-      Slot s[4];
+      Slot s[W];
       size_t n = 0;
       size_t size() const { return n; }
       Slot& operator[](size_t i) { return s[i]; }
       const Slot& operator[](size_t i) const { return s[i]; }
     };
-    // the DP's slots of wide node b: its children sharing four slots as the program chose
+    // the DP's slots of wide node b: its children sharing W slots as the program chose
     void expand(Slots& out_slots, int32_t node, int side, int budget) const {
-      const CollapseDp::SlotRef s = dp->slot_of(node, side);
+      const typename CollapseDp<W>::SlotRef s = dp->slot_of(node, side);
       if (s.code < 0) {  // a leaf of the binary tree stays a leaf
         Slot sl;
         sl.code = s.code;
@@ -694,7 +699,7 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
       expand_node(out_slots, s.code, budget);
     }
     void expand_node(Slots& out_slots, int32_t m, int budget) const {
-      const int8_t* pm = &dp->pick[static_cast<size_t>(m) * 4];
+      const int8_t* pm = &dp->pick[static_cast<size_t>(m) * W];
       while (budget > 1 && pm[budget - 1] == -1) --budget;
       if (budget == 1) {
         Slot sl;
@@ -720,19 +725,19 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
     Slots gather(int32_t b) {
       Slots slots;
       const BuildNode& n = bin.nodes[b];
-      if (dp) {  // b is a wide node: its two children share the four slots
+      if (dp) {  // b is a wide node: its two children share the W slots
         const int k = dp->wide_k[b];
         if (n.child[1] == kEmptyChild) {
-          expand(slots, b, 0, 4);
+          expand(slots, b, 0, W);
         } else {
           expand(slots, b, 0, k);
-          expand(slots, b, 1, 4 - k);
+          expand(slots, b, 1, W - k);
         }
         return slots;
       }
       for (int side = 0; side < 2; ++side)
         if (n.child[side] != kEmptyChild) slots.s[slots.n++] = slot(n, side);
-      while (slots.size() < 4) {
+      while (slots.size() < W) {
         int best = -1;
         double best_area = -1.0;
         for (size_t i = 0; i < slots.size(); ++i) {
@@ -749,9 +754,9 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
         size_t nk = 0;
         for (int side = 0; side < 2; ++side)
           if (c.child[side] != kEmptyChild) kids[nk++] = slot(c, side);
-        if (nk + slots.size() - 1 > 4) break;
+        if (nk + slots.size() - 1 > W) break;
         // replace slot `best` by the kids, in place (the order a vector erase + insert gives)
-        Slot next[4];
+        Slot next[W];
         size_t m = 0;
         for (size_t i = 0; i < slots.size(); ++i) {
           if (static_cast<int>(i) == best) {
@@ -765,18 +770,20 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
       }
       return slots;
     }
-    std::array<int32_t, 4> children(const Slots& slots, int depth, int pushes) {
+    std::array<int32_t, W> children(const Slots& slots, int depth, int pushes) {
       out->depth = std::max(out->depth, depth);
       const int here = pushes + static_cast<int>(slots.size()) - 1;
       out->max_pushes = std::max(out->max_pushes, here);
-      std::array<int32_t, 4> codes = {kEmptyChild, kEmptyChild, kEmptyChild, kEmptyChild};
+      std::array<int32_t, W> codes;
+      codes.fill(kEmptyChild);
       // the inner children of a node are allocated next to each other (then filled depth-first),
       // so the siblings a ray visits after the nearest one share its cache lines
-      int32_t slot_ids[4] = {-1, -1, -1, -1};
+      int32_t slot_ids[W];
+      std::fill(slot_ids, slot_ids + W, -1);
       for (size_t i = 0; i < slots.size(); ++i)
         if (slots[i].code >= 0) {
           slot_ids[i] = static_cast<int32_t>(out->nodes.size());
-          out->nodes.push_back(BuildNode4{});
+          out->nodes.push_back(BuildNodeW<W>{});
         }
       for (size_t i = 0; i < slots.size(); ++i)
         codes[i] = slots[i].code >= 0 ? fill(slot_ids[i], slots[i].code, depth + 1, here) : slots[i].code;
@@ -784,9 +791,9 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
     }
     int32_t fill(int32_t me, int32_t b, int depth, int pushes) {
       const Slots slots = gather(b);
-      std::array<int32_t, 4> codes = children(slots, depth, pushes);
-      BuildNode4& o = out->nodes[me];
-      for (int i = 0; i < 4; ++i) {
+      std::array<int32_t, W> codes = children(slots, depth, pushes);
+      BuildNodeW<W>& o = out->nodes[me];
+      for (int i = 0; i < W; ++i) {
         o.child[i] = codes[i];
         o.count[i] = i < static_cast<int>(slots.size()) ? slots[i].count : 0;
         for (int k = 0; k < 3; ++k) {
@@ -798,11 +805,14 @@ void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm) {
     }
   } rec{bin, out, slot_of, prm.sah ? &dp : nullptr};
   out->nodes.reserve(bin.nodes.size() / 2 + 2);
-  out->nodes.push_back(BuildNode4{});  // the root is node 0
+  out->nodes.push_back(BuildNodeW<W>{});  // the root is node 0
   rec.fill(0, 0, 1, 0);
 }
+template void collapse_bvh<4>(const Bvh&, BvhW<4>*, const CollapseParams&);
+template void collapse_bvh<8>(const Bvh&, BvhW<8>*, const CollapseParams&);
 
-void reorder_top_bfs(Bvh4* t, int64_t top) {
+template <int W>
+void reorder_top_bfs(BvhW<W>* t, int64_t top) {
   const int64_t n = static_cast<int64_t>(t->nodes.size());
   if (n <= 1 || top <= 1) return;
   // the first `top` nodes of a breadth-first walk from the root, then the rest in their (depth-first)
@@ -813,7 +823,7 @@ void reorder_top_bfs(Bvh4* t, int64_t top) {
   order.push_back(0);
   taken[0] = 1;
   for (size_t head = 0; head < order.size() && static_cast<int64_t>(order.size()) < top; ++head)
-    for (int c = 0; c < 4 && static_cast<int64_t>(order.size()) < top; ++c) {
+    for (int c = 0; c < W && static_cast<int64_t>(order.size()) < top; ++c) {
       const int32_t ch = t->nodes[order[head]].child[c];
       if (ch >= 0 && !taken[ch]) {
         taken[ch] = 1;
@@ -824,16 +834,19 @@ void reorder_top_bfs(Bvh4* t, int64_t top) {
     if (!taken[k]) order.push_back(k);
   std::vector<int32_t> pos(n);
   for (int32_t k = 0; k < n; ++k) pos[order[k]] = k;
-  std::vector<BuildNode4> out(n);
+  std::vector<BuildNodeW<W>> out(n);
   for (int32_t k = 0; k < n; ++k) {
     out[k] = t->nodes[order[k]];
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < W; ++c)
       if (out[k].child[c] >= 0) out[k].child[c] = pos[out[k].child[c]];
   }
   t->nodes.swap(out);
 }
+template void reorder_top_bfs<4>(BvhW<4>*, int64_t);
+template void reorder_top_bfs<8>(BvhW<8>*, int64_t);
 
-void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
+void hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
+  const int64_t words = 7 * width, bytes = 28 * width;  // a node: 6 plane rows + 1 code row of `width`
   std::vector<int32_t>& order = *order_out;
   order.resize(n);
   if (n <= 1) return;
@@ -843,14 +856,14 @@ void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vect
                    [&](int32_t a, int32_t b) { return visits[a] > visits[b]; });
   std::vector<int32_t> pos(n);
   for (int64_t k = 0; k < n; ++k) pos[order[k]] = static_cast<int32_t>(k);
-  std::vector<int32_t> out(static_cast<size_t>(n) * 28);
+  std::vector<int32_t> out(static_cast<size_t>(n) * words);
   for (int64_t k = 0; k < n; ++k) {
-    std::memcpy(&out[k * 28], &rec[static_cast<int64_t>(order[k]) * 28], 112);
-    int32_t* code = &out[k * 28 + 24];
-    for (int c = 0; c < 4; ++c)
-      if (code[c] >= 0) code[c] = pos[code[c] / 112] * 112;  // inner child: byte offset of its node
+    std::memcpy(&out[k * words], &rec[static_cast<int64_t>(order[k]) * words], bytes);
+    int32_t* code = &out[k * words + 6 * width];
+    for (int c = 0; c < width; ++c)
+      if (code[c] >= 0) code[c] = static_cast<int32_t>(pos[code[c] / bytes] * bytes);  // inner: byte offset
   }
-  std::memcpy(rec, out.data(), static_cast<size_t>(n) * 112);
+  std::memcpy(rec, out.data(), static_cast<size_t>(n) * bytes);
 }
 
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {

@@ -65,40 +65,56 @@ struct Bvh {
   int32_t depth = 0;
 };
 
-// 4-wide node collapsed from the binary tree (2..4 children; unused slots kEmptyChild).
-struct BuildNode4 {
-  double lo[4][3];
-  double hi[4][3];
-  int32_t child[4];  // >= 0 node index, < 0 leaf -(1 + first ref), kEmptyChild unused
-  int32_t count[4];
+// W-wide node collapsed from the binary tree (2..W children; unused slots kEmptyChild), W = 4 or 8.
+template <int W>
+struct BuildNodeW {
+  double lo[W][3];
+  double hi[W][3];
+  int32_t child[W];  // >= 0 node index, < 0 leaf -(1 + first ref), kEmptyChild unused
+  int32_t count[W];
 };
+using BuildNode4 = BuildNodeW<4>;
+using BuildNode8 = BuildNodeW<8>;
 
-struct Bvh4 {
-  std::vector<BuildNode4> nodes;
+template <int W>
+struct BvhW {
+  std::vector<BuildNodeW<W>> nodes;
   int32_t depth = 0;       // nodes on the longest root-to-leaf path
-  int32_t max_pushes = 0;  // most stack entries an ordered traversal can hold at once
+  int32_t max_pushes = 0;  // most stack entries an ordered traversal (one per sibling) can hold at once
 };
+using Bvh4 = BvhW<4>;
+using Bvh8 = BvhW<8>;
 
-// Collapse a binary child-pair BVH into a 4-wide one: greedy (open the largest-area inner child until
-// four slots are filled; leaves unchanged) or SAH-optimal (dynamic program over the binary tree; may
+// Collapse a binary child-pair BVH into a W-wide one: greedy (open the largest-area inner child until
+// W slots are filled; leaves unchanged) or SAH-optimal (dynamic program over the binary tree; may
 // merge small subtrees into leaves of up to max_leaf primitives, whose refs are contiguous).
 struct CollapseParams {
   bool sah = false;
   double c_node = 1.0;  // cost of a wide-node visit relative to one primitive test
   int max_leaf = 4;     // <= 8 (the leaf code's count field)
 };
-void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm = CollapseParams{});
+template <int W>
+void collapse_bvh(const Bvh& bin, BvhW<W>* out, const CollapseParams& prm = CollapseParams{});
+inline void collapse_bvh4(const Bvh& bin, Bvh4* out, const CollapseParams& prm = CollapseParams{}) {
+  collapse_bvh<4>(bin, out, prm);
+}
 
-// Renumber a 4-wide tree so its first `top` nodes are the top of the tree in breadth-first order
+// Renumber a W-wide tree so its first `top` nodes are the top of the tree in breadth-first order
 // (the root stays node 0; the rest keep their depth-first order). Scenes too large for LDS keep
 // that prefix in LDS (the treelet schedule), so the nodes every ray visits are ds_reads.
 constexpr int64_t kTreeletBfsNodes = 4096;
-void reorder_top_bfs(Bvh4* t, int64_t top);
-// Hot treelet (rtg_scene_prepare): renumber n device-format 4-wide nodes (112 B = 28 int32 each, codes
-// in the last 4: inner child = byte offset of its node) so the root stays first and the others follow
-// by descending visits (stable); inner codes remapped, leaf and empty codes unchanged. order_out[k] =
-// the old index of new node k.
-void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out);
+template <int W>
+void reorder_top_bfs(BvhW<W>* t, int64_t top);
+// Hot treelet (rtg_scene_prepare): renumber n device-format W-wide nodes (28 W bytes = 7 W int32 each:
+// six plane rows, then the code row; inner child = byte offset of its node) so the root stays first
+// and the others follow by descending visits (stable); inner codes remapped, leaf and empty codes
+// unchanged. order_out[k] = the old index of new node k.
+void hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out);
+inline void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
+  hot_order_nodes(rec, 4, visits, n, order_out);
+}
+// Device bytes of one node of a W-wide tree (W = 4: 112, W = 8: 224).
+constexpr int node_bytes(int width) { return 28 * width; }
 
 // aabb of one primitive exactly as the reference computes it (aabb.hpp:30-48,135-154;
 // sphere.hpp:16-44; quad.hpp:30-38).
@@ -194,6 +210,14 @@ hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int3
 
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
 
+// Ray queues of the small-scene schedule (RTG_RAY_QUEUE prototype, rtg_kernels.hip render_stream_q):
+// control words, dwords per shade-queue entry (path state + unit + hit) and per trace-queue entry, the
+// tracing waves of a 4-wave workgroup (the fourth shades)
+constexpr int kQCtl = 16;
+constexpr int kQShadeFields = 26;
+constexpr int kQTraceFields = 24;
+constexpr int kQTracerWaves = 3;
+
 // Interleaved row shards of the multi-GPU frame (rtg_shard_layout, rtg_render_frame, rtg_gather_rows):
 // rank r of N renders image rows r, r+N, ...; every shard is padded to P = ceil(H/N) rows.
 struct ShardLayout {
@@ -226,6 +250,9 @@ struct Knobs {
   int tile_slots = -1;          // RTG_TILE_SLOTS 0 (full-frame partials) | 1..65536 (-1: by chunks)
   int treelet_stack = 16;       // RTG_TREELET_STACK 4..16: LDS stack entries of the treelet schedule
                                 // (fewer: more treelet nodes, more spill traffic; spilling trees only)
+  int ray_queue = 0;            // RTG_RAY_QUEUE 0 | 1: cross-wave ray queues in the small-scene schedule
+                                // (prototype, DESIGN.md §6 "rays between waves")
+  int q_deposit = 16;           // RTG_Q_DEPOSIT 1..64: finished lanes that end a tracer wave's trips
   int treelet_hot = 1;          // RTG_TREELET_HOT 0 | 1: treelet of the most-visited nodes for the
                                 // camera (a probe render counts node visits), 0: breadth-first top
   std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
@@ -243,7 +270,8 @@ struct DevJob {
   // [6] persistent kernels' tile counter, [7] workgroups that could not run the 16-bit LDS stack
   // layout (codes past 16 bits: RTG_E_UNSUPPORTED, nothing rendered), [8..23] schedule diagnostics,
   // [24] tile-ring waits that timed out (RTG_E_INTERNAL: frame incomplete), [25] batches that found
-  // their ring slot still owned by an earlier tile (waits; diagnostic)
+  // their ring slot still owned by an earlier tile (waits; diagnostic), [26] ray-queue waits that timed
+  // out (RTG_RAY_QUEUE: RTG_E_HIP, frame incomplete)
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 64-pixel tiles per shard row of tiles
@@ -276,6 +304,12 @@ struct DevJob {
   int32_t stack_esz;                         // persistent kernels: bytes per LDS stack entry (2 or 4)
   int32_t lds_stacks;                        // persistent kernels: byte offset of the traversal stacks in LDS
   int32_t lds_ring;                          // RING kernels: byte offset of the per-wave batch tables (64 B each)
+  // ray queues (RTG_RAY_QUEUE, small-scene schedule): byte offset of the workgroup's queue area in LDS
+  // (-1: off), capacities (powers of two) of the shade queue (rays that finished traversal) and of the
+  // trace queue (shaded rays waiting for a tracer lane), the most unit contexts a workgroup keeps in
+  // flight, and the finished tracer lanes that end a tracer wave's trips
+  int32_t lds_queue;
+  int32_t q_shade, q_trace, q_rmax, q_deposit;
 
 };
 

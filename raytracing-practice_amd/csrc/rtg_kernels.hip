@@ -294,13 +294,16 @@ __device__ __forceinline__ bool at_inner(const Trav& t) {  // 0 <= todo < kTravD
   return static_cast<uint32_t>(t.todo) < static_cast<uint32_t>(kTravDone);
 }
 
+template <int WIDE = 4>
 __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 d, int32_t origin) {
   t.ix = __builtin_amdgcn_rcpf(d.x);
   t.iy = __builtin_amdgcn_rcpf(d.y);
   t.iz = __builtin_amdgcn_rcpf(d.z);
-  t.sx = (static_cast<uint32_t>(ibits(t.ix)) >> 31) * 48;
-  t.sy = (static_cast<uint32_t>(ibits(t.iy)) >> 31) * 48;
-  t.sz = (static_cast<uint32_t>(ibits(t.iz)) >> 31) * 48;
+  // byte offset of the far-plane rows (hi.x after lo.x, ...): 48 in 4-wide nodes, 96 in 8-wide ones
+  constexpr int32_t kHalf = WIDE == 8 ? 96 : 48;
+  t.sx = (static_cast<uint32_t>(ibits(t.ix)) >> 31) * kHalf;
+  t.sy = (static_cast<uint32_t>(ibits(t.iy)) >> 31) * kHalf;
+  t.sz = (static_cast<uint32_t>(ibits(t.iz)) >> 31) * kHalf;
   t.a = dot(d, d);
   t.inv_a = div_rn(1.0f, t.a);
   t.ox = -o.x * t.ix;
@@ -568,11 +571,120 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
+// ---- 8-wide nodes (RTG_BVH_WIDTH=8, the cache-read schedules; A/B of DESIGN.md §8) ----
+// Node: 224 B, rows of eight floats lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, then eight int32 codes (+192).
+// A visit tests all eight child boxes, continues with the nearest hit child and pushes ONE stack entry
+// for the rest: the node's byte offset / 32 (node offsets are multiples of 224 = 7 x 32) in the upper 24
+// bits and the 8-bit mask of its hit children not yet visited; a pop takes the lowest slot of the top
+// entry (slot order: the far children are not sorted, which r03 measured at +0.5 % box tests on 4-wide
+// nodes) and reads that child's code. The stack then holds at most one entry per tree level (config 5:
+// the tree's depth instead of the 36 sibling entries of the sorted 4-wide pushes, so no spill).
+constexpr int32_t kNode8Bytes = 224;
+
+template <int GEOM>
+__device__ __forceinline__ int32_t code8(const DevScene& S, int32_t node, int slot) {
+  if (GEOM == kGeomTreelet && node < S.treelet_bytes) return lds_ld1(S.treelet_lds + node + 192 + 4 * slot);
+  return *reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(S.nodes) + node + 192 + 4 * slot);
+}
+
+template <class Stk, int GEOM>
+__device__ __forceinline__ void trav_pop8(Trav& t, const DevScene& S, const Stk& stk) {
+  if (t.sp == 0) {
+    t.todo = kTravDone;
+    return;
+  }
+  const int32_t g = stk.load(t.sp - 1);
+  uint32_t m = static_cast<uint32_t>(g) & 255u;
+  const int32_t node = static_cast<int32_t>(static_cast<uint32_t>(g) >> 8) << 5;
+  const int slot = __builtin_ctz(m);
+  m &= m - 1u;
+  if (m != 0u)
+    stk.store(t.sp - 1, (g & ~255) | static_cast<int32_t>(m));
+  else
+    --t.sp;
+  t.todo = code8<GEOM>(S, node, slot);
+}
+
+template <class Stk, bool COUNT, int GEOM>
+__device__ __forceinline__ void node_step8(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
+                                           bool& overflow, bool& corrupt) {
+  if (t.todo >= S.node_limit) {  // corrupt child code: report, never read out of bounds
+    corrupt = true;
+    t.todo = kTravDone;
+    return;
+  }
+  if (COUNT && S.node_visits) atomicAdd(S.node_visits + t.todo / kNode8Bytes, 1u);
+  const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
+  const uint32_t na = static_cast<uint32_t>(t.todo);
+  const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
+  nf4 r[12];  // near x, y, z then far x, y, z; two halves (children 0-3, 4-7) each
+  const int32_t off[6] = {sx, 32 + sy, 64 + sz, 96 - sx, 128 - sy, 160 - sz};
+  if (GEOM == kGeomTreelet && t.todo < S.treelet_bytes) {
+    const uint32_t la = S.treelet_lds + na;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      r[2 * k] = lds_ld4(la + off[k]);
+      r[2 * k + 1] = lds_ld4(la + off[k] + 16);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      r[2 * k] = *reinterpret_cast<const nf4*>(nb + off[k]);
+      r[2 * k + 1] = *reinterpret_cast<const nf4*>(nb + off[k] + 16);
+    }
+  }
+  if (COUNT) cnt.box += 8;
+  const f2 ix = {t.ix, t.ix}, iy = {t.iy, t.iy}, iz = {t.iz, t.iz};
+  const f2 ox = {t.ox, t.ox}, oy = {t.oy, t.oy}, oz = {t.oz, t.oz};
+  // the eight children's entry / exit distances (sign-selected slab planes, as node_step4), keys of
+  // the hit ones (entry distance bits, slot in the low 3 bits) and the hit mask
+  uint32_t mask = 0u, kmin = ~0u;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const nf4 nx = r[h], ny = r[2 + h], nz = r[4 + h], fx = r[6 + h], fy = r[8 + h], fz = r[10 + h];
+    const f2 n_x[2] = {pk_fma(f2{nx.x, nx.y}, ix, ox), pk_fma(f2{nx.z, nx.w}, ix, ox)};
+    const f2 n_y[2] = {pk_fma(f2{ny.x, ny.y}, iy, oy), pk_fma(f2{ny.z, ny.w}, iy, oy)};
+    const f2 n_z[2] = {pk_fma(f2{nz.x, nz.y}, iz, oz), pk_fma(f2{nz.z, nz.w}, iz, oz)};
+    const f2 f_x[2] = {pk_fma(f2{fx.x, fx.y}, ix, ox), pk_fma(f2{fx.z, fx.w}, ix, ox)};
+    const f2 f_y[2] = {pk_fma(f2{fy.x, fy.y}, iy, oy), pk_fma(f2{fy.z, fy.w}, iy, oy)};
+    const f2 f_z[2] = {pk_fma(f2{fz.x, fz.y}, iz, oz), pk_fma(f2{fz.z, fz.w}, iz, oz)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int p = c >> 1, e = c & 1;
+      const float tn = fmaxf(fmaxf(fmaxf(n_x[p][e], n_y[p][e]), n_z[p][e]), kTMin);
+      const float tf = fminf(fminf(fminf(f_x[p][e], f_y[p][e]), f_z[p][e]), t.tbest);
+      const uint32_t slot = 4u * h + c;
+      const bool hit = tn <= tf;
+      mask |= hit ? (1u << slot) : 0u;
+      kmin = min(kmin, hit ? ((static_cast<uint32_t>(ibits(tn)) & ~7u) | slot) : ~0u);
+    }
+  }
+  if (kmin == ~0u) {
+    trav_pop8<Stk, GEOM>(t, S, stk);
+    return;
+  }
+  const int slot = static_cast<int>(kmin & 7u);
+  mask &= ~(1u << slot);
+  if (mask != 0u) {  // one entry for the node's other hit children
+    if (t.sp < stk.capacity())
+      stk.store(t.sp++, ((t.todo >> 5) << 8) | static_cast<int32_t>(mask));
+    else
+      overflow = true;
+  }
+  t.todo = code8<GEOM>(S, t.todo, slot);
+}
+
 // Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
 // LDS schedule outside the COUNT diagnostics, as for node codes).
-template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false>
+template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
+  auto pop = [&]() {
+    if constexpr (WIDE == 8)
+      trav_pop8<Stk, GEOM>(t, S, stk);
+    else
+      trav_pop(t, stk);
+  };
   const int32_t code = ~t.todo;
   const int32_t first = code >> 3;
   const int32_t count = (code & 7) + 1;
@@ -592,7 +704,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
         if (MAT) t.mat = ibits(sp4[1].w);
       }
     }
-    trav_pop(t, stk);
+    pop();
     return;
   }
   for (int k = 0; k < count; ++k) {
@@ -615,7 +727,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       if (MAT) t.mat = m;
     }
   }
-  trav_pop(t, stk);
+  pop();
 }
 
 // One unit of traversal work for this lane (used by the per-segment schedule).
@@ -1366,7 +1478,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       t_start = t;
     }
     if (fresh || cont) {
-      trav_begin(tr, S, ps.o, ps.d, ps.origin);
+      trav_begin<WIDE>(tr, S, ps.o, ps.d, ps.origin);
       if (S.occluder >= 0) {  // the scene-spanning sphere kept out of the BVH (DevScene::occluder)
         const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * S.sphere_f4;
         if (COUNT) w.cnt.prim += 1;
@@ -1416,7 +1528,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       if (leaf_trip && tr.todo < 0)
-        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt,
+                                                                           w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
@@ -1425,11 +1538,16 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
 #ifndef RTG_AB_CACHE_NODE_REPS
 #define RTG_AB_CACHE_NODE_REPS 2
 #endif
-      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : RTG_AB_CACHE_NODE_REPS;
+#ifndef RTG_AB_NODE8_REPS
+#define RTG_AB_NODE8_REPS 1
+#endif
+      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : (WIDE == 8 ? RTG_AB_NODE8_REPS : RTG_AB_CACHE_NODE_REPS);
 #pragma unroll
       for (int rep = 0; rep < kNodeReps; ++rep) {
         if (at_inner(tr)) {
-          if constexpr (WIDE == 4)
+          if constexpr (WIDE == 8)
+            node_step8<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+          else if constexpr (WIDE == 4)
             node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
           else
             node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
@@ -1508,6 +1626,387 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   if (ring && (exhausted_by_timeout || e_used != 0) && lane == 0) atomicAdd(&J.counters[24], 1ull);
 }
 
+// ---- Rays between waves (RTG_RAY_QUEUE; VERDICT r03 item 4, a prototype on the small-scene schedule) ----
+// In render_stream a wave owns its 64 rays: a lane whose traversal has finished waits, idle, until the
+// wave's shading batch, and a shading batch runs with the still-traversing lanes idle (lane utilisation
+// 0.45-0.49 on every config). Here the rays move between the waves of a workgroup through
+// two LDS queues: waves 0..2 only trace; when a few of a tracer wave's lanes have finished their
+// closest-hit query, those lanes deposit their ray (path state + hit + its unit: pixel, sample range,
+// chunk sum) in the SHADE queue and take a shaded ray from the TRACE queue (or, when that is empty, a
+// fresh unit), so tracer lanes do not wait for shading; wave 3 only shades: it takes up to 64 rays from
+// the shade queue, shades them with full waves, finishes paths and units exactly as render_stream does
+// (a unit's samples stay in order in one context, so every chunk sum is bit-identical), and puts the
+// continuing rays in the trace queue. Queues: [field][slot] dword arrays (conflict-free for consecutive
+// slots), ring indices under a workgroup lock. A workgroup keeps at most q_rmax unit contexts in flight
+// (192 tracer lanes + both queue capacities): with that many, a tracer lane can always deposit or the
+// shader can always hand rays back, so the queues never deadlock. Every wait is bounded (counters[26]).
+// control words (kQCtl): [0] lock, [1] shade head, [2] shade count, [3] trace head, [4] trace count,
+// [5] unit contexts in flight, [6] tracer waves that handed out their last unit
+
+struct RayQueues {
+  lu32* ctl;
+  lu32* sq;  // [kQShadeFields][S]
+  lu32* tq;  // [kQTraceFields][T]
+  int S, T;
+};
+
+__device__ __forceinline__ uint32_t q_ld(lu32* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void q_st(lu32* a, uint32_t v) {
+  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Workgroup lock (ctl[0]) for one wave; false when it could not be taken (bounded: counters[26]).
+__device__ __forceinline__ bool q_lock(const DevJob& J, lu32* ctl) {
+  uint32_t ok = 1;
+  if (__lane_id() == 0) {
+    uint32_t spins = 0;
+    for (;;) {
+      uint32_t expect = 0;
+      if (__hip_atomic_compare_exchange_strong(ctl, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP))
+        break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 22)) {
+        ok = 0;
+        atomicAdd(&J.counters[26], 1ull);
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+__device__ __forceinline__ void q_unlock(lu32* ctl) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (__lane_id() == 0) __hip_atomic_store(ctl, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// A unit context (its current path and the unit's own state), field by field into slot i of a queue.
+struct UnitCtx {
+  PathState ps;
+  V3 acc;
+  uint32_t px;
+  int sample, s_end, chunk;
+};
+__device__ __forceinline__ void q_put(lu32* q, int N, int i, const UnitCtx& u, bool hit, float t, int32_t best) {
+  auto put = [&](int f, uint32_t v) { q[f * N + i] = v; };
+  auto putf = [&](int f, float v) { put(f, __float_as_uint(v)); };
+  putf(0, u.ps.o.x), putf(1, u.ps.o.y), putf(2, u.ps.o.z);
+  putf(3, u.ps.d.x), putf(4, u.ps.d.y), putf(5, u.ps.d.z);
+  putf(6, u.ps.time);
+  putf(7, u.ps.T.x), putf(8, u.ps.T.y), putf(9, u.ps.T.z);
+  putf(10, u.ps.L.x), putf(11, u.ps.L.y), putf(12, u.ps.L.z);
+  put(13, static_cast<uint32_t>(u.ps.depth));
+  put(14, static_cast<uint32_t>(u.ps.origin));
+  put(15, static_cast<uint32_t>(u.ps.rng)), put(16, static_cast<uint32_t>(u.ps.rng >> 32));
+  putf(17, u.acc.x), putf(18, u.acc.y), putf(19, u.acc.z);
+  put(20, u.px);
+  put(21, static_cast<uint32_t>(u.sample) | (static_cast<uint32_t>(u.s_end) << 16));
+  put(22, static_cast<uint32_t>(u.chunk));
+  put(23, 0u);
+  if (hit) {
+    putf(24, t);
+    put(25, static_cast<uint32_t>(best));
+  }
+}
+__device__ __forceinline__ void q_get(lu32* q, int N, int i, UnitCtx& u, bool hit, float& t, int32_t& best) {
+  auto get = [&](int f) { return q[f * N + i]; };
+  auto getf = [&](int f) { return __uint_as_float(get(f)); };
+  u.ps.o = v3(getf(0), getf(1), getf(2));
+  u.ps.d = v3(getf(3), getf(4), getf(5));
+  u.ps.time = getf(6);
+  u.ps.T = v3(getf(7), getf(8), getf(9));
+  u.ps.L = v3(getf(10), getf(11), getf(12));
+  u.ps.depth = static_cast<int>(get(13));
+  u.ps.origin = static_cast<int32_t>(get(14));
+  u.ps.rng = static_cast<uint64_t>(get(15)) | (static_cast<uint64_t>(get(16)) << 32);
+  u.acc = v3(getf(17), getf(18), getf(19));
+  u.px = get(20);
+  const uint32_t se = get(21);
+  u.sample = static_cast<int>(se & 0xffffu);
+  u.s_end = static_cast<int>(se >> 16);
+  u.chunk = static_cast<int>(get(22));
+  if (hit) {
+    t = getf(24);
+    best = static_cast<int32_t>(get(25));
+  }
+}
+
+// A unit's result: its chunk partial sum (or the pixel mean when the pixel has one chunk).
+__device__ __forceinline__ void store_unit(const DevCamera& C, const DevJob& J, const UnitCtx& u) {
+  const int64_t pix = static_cast<int64_t>(px_lr(u.px)) * C.width + px_i(u.px);
+  if (J.partial == nullptr) {
+    float* o = J.out + pix * 3;
+    o[0] = C.scale * u.acc.x;
+    o[1] = C.scale * u.acc.y;
+    o[2] = C.scale * u.acc.z;
+  } else {
+    float* o = J.partial + (static_cast<int64_t>(u.chunk) * J.row_count * C.width + pix) * 3;
+    o[0] = u.acc.x;
+    o[1] = u.acc.y;
+    o[2] = u.acc.z;
+  }
+}
+
+// The shading wave: batches of up to 64 rays from the shade queue, shaded with full lanes.
+template <bool COUNT, bool TEXF>
+__device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, const DevJob& J, const RayQueues& Q,
+                                         WaveStats<COUNT>& w) {
+  const int lane = __lane_id();
+  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
+  uint32_t idle = 0;
+  for (;;) {
+    if (!q_lock(J, Q.ctl)) return;
+    const uint32_t head = q_ld(Q.ctl + 1), cnt = q_ld(Q.ctl + 2), tcnt = q_ld(Q.ctl + 4);
+    // a full batch, or what there is when no shaded ray waits for the tracers (they may be starving)
+    const uint32_t take = cnt >= 64u ? 64u : (tcnt == 0u ? cnt : 0u);
+    UnitCtx u;
+    float t = 0.0f;
+    int32_t best = -1;
+    const bool mine = static_cast<uint32_t>(lane) < take;
+    if (mine) q_get(Q.sq, Q.S, static_cast<int>((head + lane) & (Q.S - 1)), u, true, t, best);
+    if (take != 0u) {
+      if (lane == 0) {
+        q_st(Q.ctl + 1, (head + take) & (Q.S - 1));
+        q_st(Q.ctl + 2, cnt - take);
+      }
+    }
+    q_unlock(Q.ctl);
+    if (take == 0u) {
+      // done once every tracer wave has handed out its last unit and no unit is in flight
+      if (q_ld(Q.ctl + 6) >= static_cast<uint32_t>(kQTracerWaves) && q_ld(Q.ctl + 5) == 0u) return;
+      __builtin_amdgcn_s_sleep(2);
+      if (++idle > (1u << 24)) {
+        if (lane == 0) atomicAdd(&J.counters[26], 1ull);
+        return;
+      }
+      continue;
+    }
+    idle = 0;
+    bool cont = false, unit_done = false;
+    if (mine) {
+      ++w.segs;
+      bool alive_path;
+      if (best < 0) {
+        u.ps.L = vfma(u.ps.T, bg, u.ps.L);
+        alive_path = false;
+      } else {
+        if (COUNT) ++w.hits;
+        alive_path = shade<TEXF>(S, u.ps, best, t);
+        if (alive_path && --u.ps.depth <= 0) alive_path = false;
+      }
+      cont = alive_path;
+      if (!alive_path) {
+        u.acc = add(u.acc, u.ps.L);
+        ++u.sample;
+        if (u.sample < u.s_end) {
+          start_pixel_sample(u.ps, C, J, u.px, static_cast<uint32_t>(u.sample));
+          cont = true;
+        } else {
+          store_unit(C, J, u);
+          unit_done = true;
+          ++w.pixels;
+        }
+      }
+    }
+    const uint32_t ndone = static_cast<uint32_t>(__popcll(ballot(unit_done)));
+    const uint64_t pm = ballot(cont);
+    const uint32_t npush = static_cast<uint32_t>(__popcll(pm));
+    const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(pm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(pm), 0u)));
+    // the continuing rays into the trace queue (room is guaranteed by the workgroup's q_rmax; bounded wait)
+    uint32_t spins = 0;
+    while (npush != 0u) {
+      if (!q_lock(J, Q.ctl)) return;
+      const uint32_t th = q_ld(Q.ctl + 3), tc = q_ld(Q.ctl + 4);
+      const bool room = tc + npush <= static_cast<uint32_t>(Q.T);
+      if (room) {
+        if (cont) q_put(Q.tq, Q.T, static_cast<int>((th + tc + rank) & (Q.T - 1)), u, false, 0.0f, 0);
+        if (lane == 0) q_st(Q.ctl + 4, tc + npush);
+      }
+      q_unlock(Q.ctl);
+      if (room) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 22)) {
+        if (lane == 0) atomicAdd(&J.counters[26], 1ull);
+        return;
+      }
+    }
+    if (ndone != 0u && lane == 0)
+      __hip_atomic_fetch_sub(Q.ctl + 5, ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// A tracing wave: render_stream's hand-out and trip loop, with finished lanes depositing their ray in
+// the shade queue and refilling from the trace queue (then from fresh units) instead of shading.
+template <class Stk, bool COUNT, bool TEXF>
+__device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, const DevJob& J, const Stk& stk,
+                                         const RayQueues& Q, WaveStats<COUNT>& w) {
+  const int lane = __lane_id();
+  const int num_batches = J.num_tiles * J.chunks;
+  UnitCtx u;
+  u.acc = v3(0.0f, 0.0f, 0.0f);
+  u.px = 0;
+  u.sample = 0, u.s_end = 0, u.chunk = 0;
+  u.ps = {};
+  auto has = [&]() { return u.s_end != 0; };
+  bool fresh = false, arrived = false;
+  int bx = 0, by = 0, bc = 0, k_next = 64;
+  bool exhausted = false, reported = false;
+  Trav tr = {};
+  tr.todo = kTravDone;
+  uint32_t idle = 0;
+  int backlog = 0;  // finished lanes the shade queue had no room for at the last deposit
+  for (;;) {
+    // 1. deposit finished rays, refill empty lanes from the trace queue (one lock)
+    const bool fin = has() && !trav_active(tr);
+    const uint64_t fm = ballot(fin);
+    bool tq_empty = true;
+    backlog = 0;
+    if (fm != 0 || ballot(!has()) != 0) {
+      if (!q_lock(J, Q.ctl)) return;
+      const uint32_t sh = q_ld(Q.ctl + 1), sc = q_ld(Q.ctl + 2);
+      const uint32_t take = min(static_cast<uint32_t>(__popcll(fm)), static_cast<uint32_t>(Q.S) - sc);
+      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(fm >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(fm), 0u)));
+      if (fin && static_cast<uint32_t>(rank) < take) {
+        q_put(Q.sq, Q.S, static_cast<int>((sh + sc + rank) & (Q.S - 1)), u, true, tr.tbest, tr.best);
+        u.s_end = 0;  // the lane is empty now
+      }
+      const uint64_t em = ballot(!has());
+      const uint32_t th = q_ld(Q.ctl + 3), tc = q_ld(Q.ctl + 4);
+      const uint32_t take2 = min(static_cast<uint32_t>(__popcll(em)), tc);
+      const int rank2 = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(em >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(em), 0u)));
+      if (!has() && static_cast<uint32_t>(rank2) < take2) {
+        float t_unused;
+        int32_t b_unused;
+        q_get(Q.tq, Q.T, static_cast<int>((th + rank2) & (Q.T - 1)), u, false, t_unused, b_unused);
+        arrived = true;
+      }
+      if (lane == 0) {
+        q_st(Q.ctl + 2, sc + take);
+        q_st(Q.ctl + 3, (th + take2) & (Q.T - 1));
+        q_st(Q.ctl + 4, tc - take2);
+      }
+      tq_empty = tc == take2;
+      backlog = __popcll(fm) - static_cast<int>(take);
+      q_unlock(Q.ctl);
+    }
+    // 2. fresh units for lanes still empty, while the trace queue is empty and the workgroup's budget of
+    // units in flight allows (render_stream's batch hand-out)
+    uint64_t want = ballot(!has());
+    if (want != 0 && tq_empty && !(exhausted && k_next >= 64)) {
+      const uint32_t rays = q_ld(Q.ctl + 5);
+      int budget = rays < static_cast<uint32_t>(J.q_rmax) ? J.q_rmax - static_cast<int>(rays) : 0;
+      int started = 0;
+      while (want != 0 && budget > 0 && !(exhausted && k_next >= 64)) {
+        if (k_next >= 64) {
+          int b = 0;
+          if (lane == 0) b = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
+          b = __builtin_amdgcn_readfirstlane(b);
+          if (b >= num_batches) {
+            exhausted = true;
+            break;
+          }
+          const int tile = b / J.chunks;
+          bc = J.chunk_begin + (b - tile * J.chunks);
+          const int ty = tile / J.tiles_x;
+          bx = (tile - ty * J.tiles_x) << J.tile_lw;
+          by = ty << (6 - J.tile_lw);
+          k_next = 0;
+        }
+        const int take = min(min(__popcll(want), 64 - k_next), budget);
+        const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+            static_cast<uint32_t>(want >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(want), 0u)));
+        bool got = false;
+        if (!has() && rank < take) {
+          const int k = k_next + rank;
+          const int i = bx + (k & ((1 << J.tile_lw) - 1));
+          const int lr = by + (k >> J.tile_lw);
+          if (i < C.width && lr < J.row_count) {
+            u.px = static_cast<uint32_t>(i) | (static_cast<uint32_t>(lr) << 16);
+            u.chunk = bc;
+            u.sample = bc * J.chunk_samples;
+            u.s_end = min(u.sample + J.chunk_samples, C.spp);
+            u.acc = v3(0.0f, 0.0f, 0.0f);
+            fresh = true;
+            got = true;
+          }
+        }
+        const int n = __popcll(ballot(got));
+        started += n;
+        budget -= n;
+        k_next += take;
+        want = ballot(!has());
+      }
+      if (started != 0 && lane == 0)
+        __hip_atomic_fetch_add(Q.ctl + 5, static_cast<uint32_t>(started), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (exhausted && k_next >= 64 && !reported) {  // this wave hands out no more units
+      reported = true;
+      if (lane == 0) __hip_atomic_fetch_add(Q.ctl + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (fresh) start_pixel_sample(u.ps, C, J, u.px, static_cast<uint32_t>(u.sample));
+    if (fresh || arrived) {
+      trav_begin(tr, S, u.ps.o, u.ps.d, u.ps.origin);
+      if (S.occluder >= 0) {
+        const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * S.sphere_f4;
+        if (COUNT) w.cnt.prim += 1;
+        const float th = sphere_t(sp4[0], sp4[1], u.ps.o, u.ps.d, tr.a, tr.inv_a, u.ps.time, kTMin, tr.tbest,
+                                  S.occluder == u.ps.origin);
+        if (th > 0.0f) {
+          tr.tbest = th;
+          tr.best = S.occluder;
+        }
+      }
+    }
+    fresh = arrived = false;
+    const uint64_t has_m = ballot(has());
+    const bool stalled = has_m != 0 && backlog != 0 && ballot(trav_active(tr)) == 0;  // shade queue full
+    if (has_m == 0 || stalled) {  // nothing to trace: done, or wait for the shading wave
+      if (has_m == 0 && reported && q_ld(Q.ctl + 5) == 0u) return;
+      __builtin_amdgcn_s_sleep(2);
+      if (++idle > (1u << 24)) {
+        if (lane == 0) atomicAdd(&J.counters[26], 1ull);
+        return;
+      }
+      continue;
+    }
+    idle = 0;
+    // 3. trips until q_deposit lanes have finished (or no lane traverses)
+    __builtin_amdgcn_s_setprio(1);
+    for (;;) {
+      const int at_leaf = __popcll(ballot(tr.todo < 0));
+      const bool inner_left = ballot(at_inner(tr)) != 0;
+      const bool leaf_trip = at_leaf >= J.leaf_batch || !inner_left;
+      if (leaf_trip && tr.todo < 0)
+        leaf_step<Stk, COUNT, false, false>(tr, S, u.ps.o, u.ps.d, u.ps.time, stk, w.cnt, w.corrupt);
+      if (at_inner(tr)) node_step4<Stk, COUNT, kGeomLds>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+      const uint64_t trav = ballot(trav_active(tr));
+      const int ready = __popcll(ballot(!trav_active(tr)) & has_m) - backlog;
+      if (trav == 0 || ready >= J.q_deposit) break;
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
+template <class Stk, bool COUNT, bool TEXF>
+__device__ __forceinline__ void render_stream_q(const DevScene& S, const DevCamera& C, const DevJob& J,
+                                                const Stk& stk, WaveStats<COUNT>& w, lu32* qbase, int wave) {
+  RayQueues Q;
+  Q.S = J.q_shade;
+  Q.T = J.q_trace;
+  Q.ctl = qbase;
+  Q.sq = qbase + kQCtl;
+  Q.tq = Q.sq + kQShadeFields * Q.S;
+  if (wave == kQTracerWaves)
+    q_shader<COUNT, TEXF>(S, C, J, Q, w);
+  else
+    q_tracer<Stk, COUNT, TEXF>(S, C, J, stk, Q, w);
+}
+
 // Schedule 4: the same loop on a plain grid of 256-thread workgroups (scene read through the
 // caches; used when it does not fit in LDS). Waves take tiles from the same counter.
 template <int STACK, bool SPILL, bool COUNT, int WIDE, bool TEXF, bool RING>
@@ -1532,61 +2031,15 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   trace_wave(J, t0, w.pixels, lane, slot, (blockIdx.x << 8) | wave);
 }
 
-// Schedule 3 (default when the geometry fits): persistent workgroups of WAVES waves, one per CU.
-// The workgroup copies the traversal geometry (nodes, leaf refs, spheres, quads) into LDS once;
-// afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
-// L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
-// left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
-//
-// GEOM = kGeomTreelet (schedule 5, scenes too large for LDS such as the 1M-sphere field): the same
-// persistent workgroups keep only the breadth-first top of the 4-wide tree in LDS (as many nodes as
-// fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
-// through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING>
-// WAVES = 4: compiled for 5 waves per SIMD (<= 96 VGPRs) and launched with 4-wave workgroups (small
-// scenes, the dual launch's second workgroup) or 16-wave ones (book-1's main launch): one binary for
-// both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
-// the 104-register 16-wave build (dual -0.25 %, single -0.4 %, frames identical; DESIGN.md §8), so
-// the workgroup size is read at run time (kFill, wpb) instead of from WAVES.
-__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
-  const int kFill = WAVES == 4 ? static_cast<int>(blockDim.x) : WAVES * 64;  // threads of the workgroup
-  const int wpb = kFill >> 6;                                                // waves of the workgroup
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// Schedule 3's body: the whole scene in the workgroup's LDS (render_kernel_lds with GEOM = kGeomLds).
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, bool QUEUE = false>
+__device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCamera& C, const DevJob& J,
+                                                 unsigned char* smem, int kFill, int wpb, uint64_t t0, int lane,
+                                                 int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab) {
   // the whole-scene LDS schedule of 4-wide trees without a stack spill and without image / noise
   // textures keeps 16-bit stack entries (the LDS room that lets book-1 run the dual launch; the
   // textured kernels keep 32-bit ones: earth_perlin +2 % with 16-bit)
-  constexpr bool STK16 = GEOM == kGeomLds && WIDE == 4 && !SPILL && !TEXF;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  int32_t* lstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
-  int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
-  lu32* rtab = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_ring)) +
-               (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
-  if constexpr (GEOM == kGeomTreelet) {
-    float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
-    for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += kFill) l_top[k] = S.nodes[k];
-    __syncthreads();
-    DevScene L = S;
-    L.treelet_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
-                        (__attribute__((address_space(3))) unsigned char*)smem)) +
-                    static_cast<uint32_t>(J.lds_nodes);
-    WaveStats<COUNT> w;
-    if constexpr (SPILL) {
-      // the LDS part of a spilling stack is J.lds_stack (<= STACK) entries per lane: the host may keep
-      // fewer than STACK there to leave the treelet more room (RTG_TREELET_STACK)
-      const int slot = blockIdx.x * wpb + wave;
-      int32_t* tstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * J.lds_stack * 64 + lane;
-      const SpillStack<STACK> stk{tstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
-                                  J.lds_stack, J.lds_stack + J.spill_depth};
-      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, stk, w, rtab);
-    } else {
-      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
-    }
-    flush_stats<COUNT>(J, w, lane);
-    trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
-    return;
-  }
+  constexpr bool STK16 = WIDE == 4 && !SPILL && !TEXF;
   float4* l_nodes = reinterpret_cast<float4*>(smem + J.lds_nodes);
   int32_t* l_refs = reinterpret_cast<int32_t*>(smem + J.lds_refs);
   float4* l_spheres = reinterpret_cast<float4*>(smem + J.lds_spheres);
@@ -1623,6 +2076,8 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
     for (int k = threadIdx.x; k < S.num_perlins * 256; k += kFill) l_pvec[k] = S.perlin_vec[k];
     for (int k = threadIdx.x; k < S.num_perlins * 768; k += kFill) l_pperm[k] = S.perlin_perm[k];
   }
+  if (QUEUE && threadIdx.x < kQCtl)  // the ray queues start empty (RTG_RAY_QUEUE)
+    reinterpret_cast<uint32_t*>(smem + J.lds_queue)[threadIdx.x] = 0u;
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
@@ -1653,6 +2108,10 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
     render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, stk, w, rtab);
+  } else if constexpr (QUEUE && STK16 && WIDE == 4 && !RING) {
+    lu32* qb = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_queue));
+    render_stream_q<LdsStack16<STACK>, COUNT, TEXF>(L, C, J, LdsStack16<STACK>{lstk16}, w, qb,
+                                                    __builtin_amdgcn_readfirstlane(wave));
   } else if constexpr (STK16) {
     render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, LdsStack16<STACK>{lstk16}, w, rtab);
   } else {
@@ -1661,6 +2120,63 @@ __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
 }
+
+// Schedule 3 (default when the geometry fits): persistent workgroups of WAVES waves, one per CU.
+// The workgroup copies the traversal geometry (nodes, leaf refs, spheres, quads) into LDS once;
+// afterwards every node / primitive fetch of the traversal is an LDS read instead of a divergent
+// L1 gather. Each wave then pulls 8x8 pixel tiles from a global atomic counter until none are
+// left (the exit every wave reaches), so the end of the launch has no tile-granularity tail.
+//
+// GEOM = kGeomTreelet (schedule 5, scenes too large for LDS such as the 1M-sphere field): the same
+// persistent workgroups keep only the breadth-first top of the 4-wide tree in LDS (as many nodes as
+// fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
+// through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING, bool QUEUE = false>
+// WAVES = 4: compiled for 5 waves per SIMD (<= 96 VGPRs) and launched with 4-wave workgroups (small
+// scenes, the dual launch's second workgroup) or 16-wave ones (book-1's main launch): one binary for
+// both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
+// the 104-register 16-wave build (dual -0.25 %, single -0.4 %, frames identical; DESIGN.md §8), so
+// the workgroup size is read at run time (kFill, wpb) instead of from WAVES.
+__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
+  const int kFill = WAVES == 4 ? static_cast<int>(blockDim.x) : WAVES * 64;  // threads of the workgroup
+  const int wpb = kFill >> 6;                                                // waves of the workgroup
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  int32_t* lstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
+  int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
+  lu32* rtab = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_ring)) +
+               (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
+  if constexpr (GEOM == kGeomTreelet) {
+    float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
+    for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += kFill) l_top[k] = S.nodes[k];
+    __syncthreads();
+    DevScene L = S;
+    L.treelet_lds = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                        (__attribute__((address_space(3))) unsigned char*)smem)) +
+                    static_cast<uint32_t>(J.lds_nodes);
+    WaveStats<COUNT> w;
+    if constexpr (SPILL) {
+      // the LDS part of a spilling stack is J.lds_stack (<= STACK) entries per lane: the host may keep
+      // fewer than STACK there to leave the treelet more room (RTG_TREELET_STACK)
+      const int slot = blockIdx.x * wpb + wave;
+      int32_t* tstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * J.lds_stack * 64 + lane;
+      const SpillStack<STACK> stk{tstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
+                                  J.lds_stack, J.lds_stack + J.spill_depth};
+      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, stk, w, rtab);
+    } else {
+      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
+    }
+    flush_stats<COUNT>(J, w, lane);
+    trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
+  } else {
+    render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, QUEUE>(S, C, J, smem, kFill, wpb, t0, lane, wave,
+                                                                          lstk, lstk16, rtab);
+  }
+}
+
+
 
 // Schedule 1: each loop trip runs one complete closest-hit query per lane through trav_step, so
 // the wave waits for its slowest traversal every segment.
@@ -1839,8 +2355,14 @@ KernelChoice legacy_kernel(bool count, int variant) {
 
 // Schedule 5: the persistent kernel with an LDS treelet over a scene in HBM (4-wide trees only).
 KernelChoice treelet_kernel(const DevScene& S, const DevJob& J, bool count) {
-  if (S.node_width != 4 || J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves) return {};
+  if (J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves) return {};
   const bool spill = J.spill_depth > 0, tex = S.tex_full != 0, ring = J.ring_log2 >= 0 && !count;
+  if (S.node_width == 8) {  // A/B (RTG_BVH_WIDTH=8): scenes without image / noise textures
+    if (tex) return {};
+    return spill ? lds_kernel<kLdsStack, true, 8, false, kGeomTreelet>(count, ring)
+                 : lds_kernel<kLdsStack, false, 8, false, kGeomTreelet>(count, ring);
+  }
+  if (S.node_width != 4) return {};
   if (spill)
     return tex ? lds_kernel<kLdsStack, true, 4, true, kGeomTreelet>(count, ring)
                : lds_kernel<kLdsStack, true, 4, false, kGeomTreelet>(count, ring);
@@ -1867,6 +2389,16 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
     // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
     if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
       return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring, kLdsWaves * 64);
+    if (WIDE == 4 && J.lds_waves == 4 && J.lds_queue >= 0 && stk16 && !ring) {  // the ray-queue prototype
+      KernelChoice k;
+      k.fn = count ? reinterpret_cast<const void*>(
+                         &render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds, false, true>)
+                   : reinterpret_cast<const void*>(
+                         &render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds, false, true>);
+      k.block = 4 * 64;
+      k.dynamic_lds = true;
+      return k;
+    }
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU; the dual's second launch
       return tex ? lds_kernel<kLdsStack, false, WIDE, true, kGeomLds, 4>(count, ring)
                  : lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring);
@@ -1885,6 +2417,7 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
 // The kernel a render of this plan runs (fn == nullptr: no kernel fits the plan).
 KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool count, int variant) {
   if (variant == 5) return treelet_kernel(S, J, count);
+  if (S.node_width == 8) return {};  // 8-wide trees: the treelet schedule only (A/B)
   if (variant == 3 || variant == 0)
     return S.node_width == 4 ? default_kernel<4>(S, J, count, stack, variant == 3)
                              : default_kernel<2>(S, J, count, stack, variant == 3);
@@ -1945,6 +2478,7 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   // the node array first (at LDS address 0: inner-node codes are its byte offsets, <= 15 bits for
   // trees of <= 292 4-wide nodes, LdsStack16), then the traversal stacks (esz bytes per entry)
   const int64_t nodes = 0;
+  if (S.node_width == 8) return -1;  // 8-wide trees: the treelet schedule only (A/B)
   int64_t off = a16(S.num_nodes * (S.node_width == 4 ? 112 : 64));
   const int64_t stacks = off;
   off = a16(off + int64_t(waves) * stack * 64 * esz);
@@ -1986,13 +2520,14 @@ int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
   const int64_t stacks = int64_t(waves) * stack * 64 * 4;
   const int64_t ring = J->ring_log2 >= 0 ? int64_t(waves) * kRingEntries * 4 : 0;  // RING: batch tables
   const int64_t room = 160 * 1024 - stacks - ring;
-  if (S->node_width != 4 || room < 112) return -1;
-  const int64_t nodes = std::min<int64_t>(S->num_nodes, room / 112);
-  S->treelet_bytes = static_cast<int32_t>(nodes * 112);
+  const int64_t nb = node_bytes(S->node_width);
+  if (S->node_width < 4 || room < nb) return -1;
+  const int64_t nodes = std::min<int64_t>(S->num_nodes, room / nb);
+  S->treelet_bytes = static_cast<int32_t>(nodes * nb);
   J->lds_ring = static_cast<int32_t>(stacks);
   J->lds_nodes = static_cast<int32_t>(stacks + ring);
   J->lds_stacks = 0;
-  return static_cast<int>(stacks + ring + nodes * 112);
+  return static_cast<int>(stacks + ring + nodes * nb);
 }
 
 // The dual launch (rtg_api.cpp) needs the 16-wave workgroup's four waves and the 4-wave workgroup's

@@ -117,7 +117,8 @@ class rtg_launch_plan(C.Structure):
         "lds_stack_entries", "spill_entries", "treelet_nodes", "shade_batch", "leaf_batch", "chunk_samples",
         "chunks")] + [("partial_bytes", C.c_int64), ("num_cus", C.c_int32), ("tile_slots", C.c_int32),
                       ("treelet_hot", C.c_int32), ("treelet_tune_us", C.c_int32),
-                      ("treelet_visit_permille", C.c_int32), ("reserved_", C.c_int32 * 3)]
+                      ("treelet_visit_permille", C.c_int32), ("ray_queue", C.c_int32),
+                      ("node_width", C.c_int32), ("reserved_", C.c_int32 * 1)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved_"}

@@ -78,7 +78,8 @@ def main():
         name, spec = (head.split("@", 1) if "@" in head else (first, head))
         nums = tuple(int(x) for x in (spec.split(":") + ["0", "0"])[:3])
         variants.append((name, nums, tune, env))
-        envs[variants[-1]] = dict(kv.split("=", 1) for kv in env.split(";") if kv)
+        # ";" or "^" between variables ("^" survives a shell command line unquoted)
+        envs[variants[-1]] = dict(kv.split("=", 1) for kv in env.replace("^", ";").split(";") if kv)
     times = {v: [] for v in variants}
     frames, segs, counts = {}, {}, {}
     for r in range(a.rounds):

@@ -1,0 +1,43 @@
+#!/bin/bash
+# tools/gpu_r04.sh OUTDIR STEP... — one GPU-box session (through gpurun, from the repo root). Steps:
+#   tests           pytest -m gpu (failures reported, the session goes on; a crash or timeout ends it)
+#   bench:N         bench.py --config N (BENCH_ARGS appended)
+#   ab5w8           config 5, 4-wide vs 8-wide nodes, same box, interleaved (tools/ab_schedule.py)
+#   ab:NAME:ARGS    tools/ab_schedule.py with ARGS (spaces as '+')
+# Each step runs under its own time limit; results in gpurun_out/OUTDIR/.
+set -u
+OUT=gpurun_out/${1:-session}
+shift || true
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name timeout-seconds command...
+  local name=$1 t=$2
+  shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 8 "$OUT/$name.log"
+  return $rc
+}
+for s in "$@"; do
+  case $s in
+    tests)
+      step gpu_tests 900 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
+      rc=$?
+      [ $rc -gt 1 ] && exit $rc ;;
+    bench:*)
+      c=${s#bench:}
+      step bench_config$c 700 python3 bench.py --config "$c" ${BENCH_ARGS:-} || exit $?
+      grep '^{' "$OUT/bench_config$c.log" > "$OUT/bench_config$c.json" ;;
+    ab5w8)
+      step ab5w8 700 python3 tools/ab_schedule.py --rounds 2 --grid 500 --width 3840 --spp 1000 --count \
+        --variants '0:0:0,0:0:0!RTG_BVH_WIDTH=8' || exit $? ;;
+    ab:*)
+      rest=${s#ab:}
+      name=${rest%%:*}
+      args=${rest#*:}
+      step "ab_$name" 700 python3 tools/ab_schedule.py ${args//+/ } || exit $? ;;
+  esac
+done
+exit 0

@@ -237,6 +237,7 @@ Knobs read_knobs() {
   num("RTG_TREELET_HOT", 0, 1, &k.treelet_hot);
   num("RTG_RAY_QUEUE", 0, 1, &k.ray_queue);
   num("RTG_Q_DEPOSIT", 1, 64, &k.q_deposit);
+  num("RTG_Q_SHADERS", 1, 8, &k.q_shaders);
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -291,9 +292,66 @@ bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
   std::vector<int> bad(host_threads(nn), 0);  // 1: a node without children, 2: a leaf not encodable
   host_par_for(nn, [&](int64_t b, int64_t e, int th) {
     for (int64_t k = b; k < e && !bad[th]; ++k) {
-      const BuildNodeW<W>& n = t.nodes[k];
+      const BuildNodeW<W>& n0 = t.nodes[k];
+#ifdef RTG_AB_W8_OCT
+      // A/B: octant-ordered child slots (Ylitie et al. 2017): slot s holds the child met first by rays of
+      // direction-sign octant s (bit a set: axis a negative), assigned greedily by dot(centre offset, octant)
+      BuildNodeW<W> n = n0;
+      constexpr double kInfD = std::numeric_limits<double>::infinity();
+      if (W == 8) {
+        double P[3] = {0, 0, 0};
+        int nc = 0;
+        for (int c = 0; c < W; ++c)
+          if (n0.child[c] != kEmptyChild) {
+            ++nc;
+            for (int a = 0; a < 3; ++a) P[a] += 0.5 * (n0.lo[c][a] + n0.hi[c][a]);
+          }
+        for (int a = 0; a < 3; ++a) P[a] /= nc;
+        struct Pair {
+          double cost;
+          int c, s;
+        };
+        std::vector<Pair> pairs;
+        for (int c = 0; c < W; ++c) {
+          if (n0.child[c] == kEmptyChild) continue;
+          for (int sl = 0; sl < W; ++sl) {
+            double cst = 0.0;
+            for (int a = 0; a < 3; ++a)
+              cst += (0.5 * (n0.lo[c][a] + n0.hi[c][a]) - P[a]) * ((sl >> a) & 1 ? -1.0 : 1.0);
+            pairs.push_back({cst, c, sl});
+          }
+        }
+        std::stable_sort(pairs.begin(), pairs.end(), [](const Pair& x, const Pair& y) { return x.cost < y.cost; });
+        int slot_of[W], child_in[W];
+        std::fill(slot_of, slot_of + W, -1);
+        std::fill(child_in, child_in + W, -1);
+        for (const Pair& q : pairs)
+          if (slot_of[q.c] < 0 && child_in[q.s] < 0) slot_of[q.c] = q.s, child_in[q.s] = q.c;
+        for (int sl = 0; sl < W; ++sl) {
+          const int c = child_in[sl];
+          n.child[sl] = c >= 0 ? n0.child[c] : kEmptyChild;
+          n.count[sl] = c >= 0 ? n0.count[c] : 0;
+          for (int a = 0; a < 3; ++a) {
+            n.lo[sl][a] = c >= 0 ? n0.lo[c][a] : kInfD;
+            n.hi[sl][a] = c >= 0 ? n0.hi[c][a] : -kInfD;
+          }
+        }
+        if (n.child[0] == kEmptyChild) {  // slot 0 must be a child (the empty-node check below)
+          for (int sl = 1; sl < W; ++sl)
+            if (n.child[sl] != kEmptyChild) {
+              std::swap(n.child[0], n.child[sl]);
+              std::swap(n.count[0], n.count[sl]);
+              std::swap(n.lo[0], n.lo[sl]);
+              std::swap(n.hi[0], n.hi[sl]);
+              break;
+            }
+        }
+      }
+#else
+      const BuildNodeW<W>& n = n0;
+#endif
       float* f = &out->nodes[k * kWords];
-      if (n.child[0] == kEmptyChild) {
+      if (n0.child[0] == kEmptyChild) {
         bad[th] = 1;
         break;
       }
@@ -1321,24 +1379,32 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     j4.lds_ring = l4[9];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
-  // ray queues (RTG_RAY_QUEUE prototype): the small-scene schedule (five 4-wave
-  // workgroups per CU, 16-bit stacks, no image / noise textures) of one-shot frames without the tile
-  // ring; the queues go after the scene copy, as large as five workgroups per CU still allow
-  if (K.ray_queue && variant == 3 && dj.lds_waves == 4 && lds_wgs == kSmallSceneWgs && lds4 < 0 &&
-      dj.stack_esz == 2 && !dscene.tex_full && dj.ring_log2 < 0 && !P->skip_kernel) {
+  // ray queues (RTG_RAY_QUEUE prototype) on the LDS schedule with 16-bit stacks, no image /
+  // noise textures, one-shot frames without the tile ring: the small-scene shape (five 4-wave workgroups
+  // per CU: three tracing waves + one shading wave each), or one 16-wave workgroup per CU whose queues
+  // take the LDS of the dual launch's second workgroup (book-1: 16 - RTG_Q_SHADERS tracing waves). The
+  // queues go after the scene copy, as large as the shape still allows.
+  if (K.ray_queue && variant == 3 && dj.stack_esz == 2 && !dscene.tex_full && dj.ring_log2 < 0 && !P->skip_kernel) {
     const int qoff = (lds_bytes + 15) & ~15;
-    for (const int T : {128, 64, 32}) {
-      const int Sq = 64;
-      const int qbytes = (kQCtl + kQShadeFields * Sq + kQTraceFields * T) * 4;
-      if (lds_alloc(qoff + qbytes) * kSmallSceneWgs <= kLdsPerCu) {
-        dj.lds_queue = qoff;
-        dj.q_shade = Sq;
-        dj.q_trace = T;
-        dj.q_rmax = kQTracerWaves * 64 + Sq + T;  // no queue deadlock below this (rtg_kernels.hip)
-        dj.q_deposit = K.q_deposit;
-        lds_bytes = qoff + qbytes;
-        break;
-      }
+    const bool small = dj.lds_waves == 4 && lds_wgs == kSmallSceneWgs && lds4 < 0;
+    const bool big = dj.lds_waves == kLdsWaves && lds_wgs == 1;
+    const int tracers = small ? kQTracerWaves : kLdsWaves - K.q_shaders;
+    const int Sq = small ? 64 : 128;
+    for (const int T : {512, 256, 128, 64, 32}) {
+      if (!small && !big) break;
+      const int qbytes = (kQCtl + kQEntryDw * (Sq + T)) * 4;
+      const bool fits = small ? lds_alloc(qoff + qbytes) * kSmallSceneWgs <= kLdsPerCu
+                              : lds_alloc(qoff + qbytes) <= kLdsPerCu;
+      if (!fits || (small && T > 128)) continue;
+      dj.lds_queue = qoff;
+      dj.q_shade = Sq;
+      dj.q_trace = T;
+      dj.q_tracers = tracers;
+      dj.q_rmax = tracers * 64 + Sq + T;  // no queue deadlock below this (rtg_kernels.hip)
+      dj.q_deposit = K.q_deposit;
+      lds_bytes = qoff + qbytes;
+      lds4 = -1;  // the queues replace the dual launch's second workgroup
+      break;
     }
   }
   P->j4 = j4;

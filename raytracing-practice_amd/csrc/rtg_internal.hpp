@@ -211,12 +211,11 @@ hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int3
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
 
 // Ray queues of the small-scene schedule (RTG_RAY_QUEUE prototype, rtg_kernels.hip render_stream_q):
-// control words, dwords per shade-queue entry (path state + unit + hit) and per trace-queue entry, the
-// tracing waves of a 4-wave workgroup (the fourth shades)
+// control words (16 B aligned: the entries follow them), dwords per queue entry (path state + unit +
+// hit), the tracing waves of a 4-wave workgroup (the fourth shades)
 constexpr int kQCtl = 16;
-constexpr int kQShadeFields = 26;
-constexpr int kQTraceFields = 24;
-constexpr int kQTracerWaves = 3;
+constexpr int kQEntryDw = 28;  // 112 B per queue entry (seven 16-B rows; the trace queue leaves row 6 unused)
+constexpr int kQTracerWaves = 3;  // of a 4-wave workgroup (small scenes); 16-wave ones: 16 - RTG_Q_SHADERS
 
 // Interleaved row shards of the multi-GPU frame (rtg_shard_layout, rtg_render_frame, rtg_gather_rows):
 // rank r of N renders image rows r, r+N, ...; every shard is padded to P = ceil(H/N) rows.
@@ -253,6 +252,7 @@ struct Knobs {
   int ray_queue = 0;            // RTG_RAY_QUEUE 0 | 1: cross-wave ray queues in the small-scene schedule
                                 // (prototype, DESIGN.md §6 "rays between waves")
   int q_deposit = 16;           // RTG_Q_DEPOSIT 1..64: finished lanes that end a tracer wave's trips
+  int q_shaders = 4;            // RTG_Q_SHADERS 1..8: shading waves of a 16-wave ray-queue workgroup
   int treelet_hot = 1;          // RTG_TREELET_HOT 0 | 1: treelet of the most-visited nodes for the
                                 // camera (a probe render counts node visits), 0: breadth-first top
   std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
@@ -310,6 +310,7 @@ struct DevJob {
   // flight, and the finished tracer lanes that end a tracer wave's trips
   int32_t lds_queue;
   int32_t q_shade, q_trace, q_rmax, q_deposit;
+  int32_t q_tracers;  // waves 0 .. q_tracers - 1 trace, the others shade
 
 };
 

@@ -587,6 +587,13 @@ __device__ __forceinline__ int32_t code8(const DevScene& S, int32_t node, int sl
   return *reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(S.nodes) + node + 192 + 4 * slot);
 }
 
+#ifdef RTG_AB_W8_OCT
+// the ray's direction-sign octant (bit a: axis a negative), from the far-plane row offsets (0 or 96)
+__device__ __forceinline__ int oct8(const Trav& t) {
+  return (t.sx != 0 ? 1 : 0) | (t.sy != 0 ? 2 : 0) | (t.sz != 0 ? 4 : 0);
+}
+#endif
+
 template <class Stk, int GEOM>
 __device__ __forceinline__ void trav_pop8(Trav& t, const DevScene& S, const Stk& stk) {
   if (t.sp == 0) {
@@ -596,13 +603,17 @@ __device__ __forceinline__ void trav_pop8(Trav& t, const DevScene& S, const Stk&
   const int32_t g = stk.load(t.sp - 1);
   uint32_t m = static_cast<uint32_t>(g) & 255u;
   const int32_t node = static_cast<int32_t>(static_cast<uint32_t>(g) >> 8) << 5;
-  const int slot = __builtin_ctz(m);
+  const int p = __builtin_ctz(m);
   m &= m - 1u;
   if (m != 0u)
     stk.store(t.sp - 1, (g & ~255) | static_cast<int32_t>(m));
   else
     --t.sp;
-  t.todo = code8<GEOM>(S, node, slot);
+#ifdef RTG_AB_W8_OCT  // the entry's mask is in octant order: position p is slot p ^ octant
+  t.todo = code8<GEOM>(S, node, p ^ oct8(t));
+#else
+  t.todo = code8<GEOM>(S, node, p);
+#endif
 }
 
 template <class Stk, bool COUNT, int GEOM>
@@ -665,6 +676,14 @@ __device__ __forceinline__ void node_step8(Trav& t, const DevScene& S, const Stk
   }
   const int slot = static_cast<int>(kmin & 7u);
   mask &= ~(1u << slot);
+#ifdef RTG_AB_W8_OCT  // the other hit children in octant order (bit p = slot p ^ octant): XOR the bit index
+  {
+    const int o = oct8(t);
+    if (o & 1) mask = ((mask & 0x55u) << 1) | ((mask >> 1) & 0x55u);
+    if (o & 2) mask = ((mask & 0x33u) << 2) | ((mask >> 2) & 0x33u);
+    if (o & 4) mask = ((mask & 0x0fu) << 4) | ((mask >> 4) & 0x0fu);
+  }
+#endif
   if (mask != 0u) {  // one entry for the node's other hit children
     if (t.sp < stk.capacity())
       stk.store(t.sp++, ((t.todo >> 5) << 8) | static_cast<int32_t>(mask));
@@ -1636,8 +1655,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
 // fresh unit), so tracer lanes do not wait for shading; wave 3 only shades: it takes up to 64 rays from
 // the shade queue, shades them with full waves, finishes paths and units exactly as render_stream does
 // (a unit's samples stay in order in one context, so every chunk sum is bit-identical), and puts the
-// continuing rays in the trace queue. Queues: [field][slot] dword arrays (conflict-free for consecutive
-// slots), ring indices under a workgroup lock. A workgroup keeps at most q_rmax unit contexts in flight
+// continuing rays in the trace queue. Queues: 112-B entries (seven 16-B rows, conflict-free for
+// consecutive slots), ring indices under a workgroup lock. A workgroup keeps at most q_rmax unit contexts in flight
 // (192 tracer lanes + both queue capacities): with that many, a tracer lane can always deposit or the
 // shader can always hand rays back, so the queues never deadlock. Every wait is bounded (counters[26]).
 // control words (kQCtl): [0] lock, [1] shade head, [2] shade count, [3] trace head, [4] trace count,
@@ -1645,8 +1664,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
 
 struct RayQueues {
   lu32* ctl;
-  lu32* sq;  // [kQShadeFields][S]
-  lu32* tq;  // [kQTraceFields][T]
+  lu32* sq;  // S entries of kQEntryDw dwords
+  lu32* tq;  // T entries
   int S, T;
 };
 
@@ -1682,54 +1701,56 @@ __device__ __forceinline__ void q_unlock(lu32* ctl) {
   if (__lane_id() == 0) __hip_atomic_store(ctl, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// A unit context (its current path and the unit's own state), field by field into slot i of a queue.
+// A unit context (its current path and the unit's own state) in slot i of a queue: seven 16-B rows per
+// entry (112 B, an odd number of 16-B bank slots, so the ds_write_b128 / ds_read_b128 of consecutive
+// slots spread over every bank; 7 LDS operations per copy instead of 26)
+//   row 0: o.xyz d.x | 1: d.yz time T.x | 2: T.yz L.xy | 3: L.z depth origin rng.lo
+//   row 4: rng.hi acc.xyz | 5: px (sample | s_end << 16) chunk tbest | 6: best (shade queue only)
 struct UnitCtx {
   PathState ps;
   V3 acc;
   uint32_t px;
   int sample, s_end, chunk;
 };
-__device__ __forceinline__ void q_put(lu32* q, int N, int i, const UnitCtx& u, bool hit, float t, int32_t best) {
-  auto put = [&](int f, uint32_t v) { q[f * N + i] = v; };
-  auto putf = [&](int f, float v) { put(f, __float_as_uint(v)); };
-  putf(0, u.ps.o.x), putf(1, u.ps.o.y), putf(2, u.ps.o.z);
-  putf(3, u.ps.d.x), putf(4, u.ps.d.y), putf(5, u.ps.d.z);
-  putf(6, u.ps.time);
-  putf(7, u.ps.T.x), putf(8, u.ps.T.y), putf(9, u.ps.T.z);
-  putf(10, u.ps.L.x), putf(11, u.ps.L.y), putf(12, u.ps.L.z);
-  put(13, static_cast<uint32_t>(u.ps.depth));
-  put(14, static_cast<uint32_t>(u.ps.origin));
-  put(15, static_cast<uint32_t>(u.ps.rng)), put(16, static_cast<uint32_t>(u.ps.rng >> 32));
-  putf(17, u.acc.x), putf(18, u.acc.y), putf(19, u.acc.z);
-  put(20, u.px);
-  put(21, static_cast<uint32_t>(u.sample) | (static_cast<uint32_t>(u.s_end) << 16));
-  put(22, static_cast<uint32_t>(u.chunk));
-  put(23, 0u);
-  if (hit) {
-    putf(24, t);
-    put(25, static_cast<uint32_t>(best));
-  }
+typedef unsigned int qu4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void q_row_st(lu32* q, int i, int r, qu4 v) {
+  *reinterpret_cast<__attribute__((address_space(3))) qu4*>(q + (i * kQEntryDw + 4 * r)) = v;
 }
-__device__ __forceinline__ void q_get(lu32* q, int N, int i, UnitCtx& u, bool hit, float& t, int32_t& best) {
-  auto get = [&](int f) { return q[f * N + i]; };
-  auto getf = [&](int f) { return __uint_as_float(get(f)); };
-  u.ps.o = v3(getf(0), getf(1), getf(2));
-  u.ps.d = v3(getf(3), getf(4), getf(5));
-  u.ps.time = getf(6);
-  u.ps.T = v3(getf(7), getf(8), getf(9));
-  u.ps.L = v3(getf(10), getf(11), getf(12));
-  u.ps.depth = static_cast<int>(get(13));
-  u.ps.origin = static_cast<int32_t>(get(14));
-  u.ps.rng = static_cast<uint64_t>(get(15)) | (static_cast<uint64_t>(get(16)) << 32);
-  u.acc = v3(getf(17), getf(18), getf(19));
-  u.px = get(20);
-  const uint32_t se = get(21);
-  u.sample = static_cast<int>(se & 0xffffu);
-  u.s_end = static_cast<int>(se >> 16);
-  u.chunk = static_cast<int>(get(22));
+__device__ __forceinline__ qu4 q_row_ld(lu32* q, int i, int r) {
+  return *reinterpret_cast<__attribute__((address_space(3))) const qu4*>(q + (i * kQEntryDw + 4 * r));
+}
+__device__ __forceinline__ void q_put(lu32* q, int i, const UnitCtx& u, bool hit, float t, int32_t best) {
+  auto f = [](float x) { return __float_as_uint(x); };
+  q_row_st(q, i, 0, qu4{f(u.ps.o.x), f(u.ps.o.y), f(u.ps.o.z), f(u.ps.d.x)});
+  q_row_st(q, i, 1, qu4{f(u.ps.d.y), f(u.ps.d.z), f(u.ps.time), f(u.ps.T.x)});
+  q_row_st(q, i, 2, qu4{f(u.ps.T.y), f(u.ps.T.z), f(u.ps.L.x), f(u.ps.L.y)});
+  q_row_st(q, i, 3, qu4{f(u.ps.L.z), static_cast<uint32_t>(u.ps.depth), static_cast<uint32_t>(u.ps.origin),
+                        static_cast<uint32_t>(u.ps.rng)});
+  q_row_st(q, i, 4, qu4{static_cast<uint32_t>(u.ps.rng >> 32), f(u.acc.x), f(u.acc.y), f(u.acc.z)});
+  q_row_st(q, i, 5, qu4{u.px, static_cast<uint32_t>(u.sample) | (static_cast<uint32_t>(u.s_end) << 16),
+                        static_cast<uint32_t>(u.chunk), f(t)});
+  if (hit) q_row_st(q, i, 6, qu4{static_cast<uint32_t>(best), 0u, 0u, 0u});
+}
+__device__ __forceinline__ void q_get(lu32* q, int i, UnitCtx& u, bool hit, float& t, int32_t& best) {
+  auto f = [](uint32_t x) { return __uint_as_float(x); };
+  const qu4 r0 = q_row_ld(q, i, 0), r1 = q_row_ld(q, i, 1), r2 = q_row_ld(q, i, 2), r3 = q_row_ld(q, i, 3);
+  const qu4 r4 = q_row_ld(q, i, 4), r5 = q_row_ld(q, i, 5);
+  u.ps.o = v3(f(r0.x), f(r0.y), f(r0.z));
+  u.ps.d = v3(f(r0.w), f(r1.x), f(r1.y));
+  u.ps.time = f(r1.z);
+  u.ps.T = v3(f(r1.w), f(r2.x), f(r2.y));
+  u.ps.L = v3(f(r2.z), f(r2.w), f(r3.x));
+  u.ps.depth = static_cast<int>(r3.y);
+  u.ps.origin = static_cast<int32_t>(r3.z);
+  u.ps.rng = static_cast<uint64_t>(r3.w) | (static_cast<uint64_t>(r4.x) << 32);
+  u.acc = v3(f(r4.y), f(r4.z), f(r4.w));
+  u.px = r5.x;
+  u.sample = static_cast<int>(r5.y & 0xffffu);
+  u.s_end = static_cast<int>(r5.y >> 16);
+  u.chunk = static_cast<int>(r5.z);
   if (hit) {
-    t = getf(24);
-    best = static_cast<int32_t>(get(25));
+    t = f(r5.w);
+    best = static_cast<int32_t>(q_row_ld(q, i, 6).x);
   }
 }
 
@@ -1765,7 +1786,7 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
     float t = 0.0f;
     int32_t best = -1;
     const bool mine = static_cast<uint32_t>(lane) < take;
-    if (mine) q_get(Q.sq, Q.S, static_cast<int>((head + lane) & (Q.S - 1)), u, true, t, best);
+    if (mine) q_get(Q.sq, static_cast<int>((head + lane) & (Q.S - 1)), u, true, t, best);
     if (take != 0u) {
       if (lane == 0) {
         q_st(Q.ctl + 1, (head + take) & (Q.S - 1));
@@ -1775,7 +1796,7 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
     q_unlock(Q.ctl);
     if (take == 0u) {
       // done once every tracer wave has handed out its last unit and no unit is in flight
-      if (q_ld(Q.ctl + 6) >= static_cast<uint32_t>(kQTracerWaves) && q_ld(Q.ctl + 5) == 0u) return;
+      if (q_ld(Q.ctl + 6) >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
       __builtin_amdgcn_s_sleep(2);
       if (++idle > (1u << 24)) {
         if (lane == 0) atomicAdd(&J.counters[26], 1ull);
@@ -1822,7 +1843,7 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
       const uint32_t th = q_ld(Q.ctl + 3), tc = q_ld(Q.ctl + 4);
       const bool room = tc + npush <= static_cast<uint32_t>(Q.T);
       if (room) {
-        if (cont) q_put(Q.tq, Q.T, static_cast<int>((th + tc + rank) & (Q.T - 1)), u, false, 0.0f, 0);
+        if (cont) q_put(Q.tq, static_cast<int>((th + tc + rank) & (Q.T - 1)), u, false, 0.0f, 0);
         if (lane == 0) q_st(Q.ctl + 4, tc + npush);
       }
       q_unlock(Q.ctl);
@@ -1871,7 +1892,7 @@ __device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, 
       const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(fm >> 32),
                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(fm), 0u)));
       if (fin && static_cast<uint32_t>(rank) < take) {
-        q_put(Q.sq, Q.S, static_cast<int>((sh + sc + rank) & (Q.S - 1)), u, true, tr.tbest, tr.best);
+        q_put(Q.sq, static_cast<int>((sh + sc + rank) & (Q.S - 1)), u, true, tr.tbest, tr.best);
         u.s_end = 0;  // the lane is empty now
       }
       const uint64_t em = ballot(!has());
@@ -1882,7 +1903,7 @@ __device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, 
       if (!has() && static_cast<uint32_t>(rank2) < take2) {
         float t_unused;
         int32_t b_unused;
-        q_get(Q.tq, Q.T, static_cast<int>((th + rank2) & (Q.T - 1)), u, false, t_unused, b_unused);
+        q_get(Q.tq, static_cast<int>((th + rank2) & (Q.T - 1)), u, false, t_unused, b_unused);
         arrived = true;
       }
       if (lane == 0) {
@@ -2000,8 +2021,8 @@ __device__ __forceinline__ void render_stream_q(const DevScene& S, const DevCame
   Q.T = J.q_trace;
   Q.ctl = qbase;
   Q.sq = qbase + kQCtl;
-  Q.tq = Q.sq + kQShadeFields * Q.S;
-  if (wave == kQTracerWaves)
+  Q.tq = Q.sq + kQEntryDw * Q.S;
+  if (wave >= J.q_tracers)
     q_shader<COUNT, TEXF>(S, C, J, Q, w);
   else
     q_tracer<Stk, COUNT, TEXF>(S, C, J, stk, Q, w);
@@ -2386,19 +2407,19 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
     if (J.stack_esz != (stk16 ? 2 : 4)) return {};
     if (spill || (WIDE == 4 && !tex && !stk16))
       return tex ? lds_kernel<kLdsStack, true, WIDE, true>(count, ring) : lds_kernel<kLdsStack, true, WIDE, false>(count, ring);
-    // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
-    if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
-      return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring, kLdsWaves * 64);
-    if (WIDE == 4 && J.lds_waves == 4 && J.lds_queue >= 0 && stk16 && !ring) {  // the ray-queue prototype
+    if (WIDE == 4 && J.lds_queue >= 0 && stk16 && !ring) {  // the ray-queue prototype (4- or 16-wave workgroups)
       KernelChoice k;
       k.fn = count ? reinterpret_cast<const void*>(
                          &render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds, false, true>)
                    : reinterpret_cast<const void*>(
                          &render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds, false, true>);
-      k.block = 4 * 64;
+      k.block = J.lds_waves * 64;
       k.dynamic_lds = true;
       return k;
     }
+    // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
+    if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
+      return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring, kLdsWaves * 64);
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU; the dual's second launch
       return tex ? lds_kernel<kLdsStack, false, WIDE, true, kGeomLds, 4>(count, ring)
                  : lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring);

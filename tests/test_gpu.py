@@ -645,10 +645,11 @@ def test_exact_t_ties_match_oracle(gpu_lib, oracle, bvh):
 
 
 @pytest.mark.parametrize("name,W,spp,depth", [("cornell_box", 64, 16, 100), ("cornell_box", 48, 40, 50),
-                                               ("quads", 64, 8, 50), ("checkered_spheres", 64, 8, 20)])
+                                               ("quads", 64, 8, 50), ("checkered_spheres", 64, 8, 20),
+                                               ("bouncing_spheres", 96, 8, 30), ("bouncing_spheres", 64, 40, 50)])
 def test_ray_queue_matches_oracle(gpu_lib, scenes, oracle, monkeypatch, name, W, spp, depth):
     """RTG_RAY_QUEUE=1 (the cross-wave prototype): rays move between the waves of a
-    workgroup through LDS queues (three tracing waves, one shading wave). A unit's samples stay in one
+    workgroup through LDS queues (tracing waves and shading waves). A unit's samples stay in one
     context, in order, so the frame and the segment count are cpu_ref32's and the per-wave schedule's,
     bit for bit; 40 spp covers chunked units (partial sums in chunk order)."""
     s = scenes.build(name, rand_seed=1)
@@ -662,7 +663,9 @@ def test_ray_queue_matches_oracle(gpu_lib, scenes, oracle, monkeypatch, name, W,
     ds = gpu_lib.scene_create(s.desc)  # knobs are read once per scene
     monkeypatch.delenv("RTG_RAY_QUEUE")
     p = ds.plan(c)
-    assert p.ray_queue > 0 and p.waves_per_workgroup == 4 and p.schedule == 3, p.as_dict()
+    # small scenes: five 4-wave workgroups per CU; book-1: one 16-wave workgroup (no dual launch)
+    assert p.ray_queue > 0 and p.schedule == 3 and p.dual == 0, p.as_dict()
+    assert p.waves_per_workgroup == (16 if name == "bouncing_spheres" else 4), p.as_dict()
     g, st = ds.render_host(c)
     gc, stc = ds.render_host(c, count=True)
     ds.close()

@@ -33,6 +33,35 @@ for s in "$@"; do
     ab5w8)
       step ab5w8 700 python3 tools/ab_schedule.py --rounds 2 --grid 500 --width 3840 --spp 1000 --count \
         --variants '0:0:0,0:0:0!RTG_BVH_WIDTH=8' || exit $? ;;
+    prof:*)  # prof:NAME:CONFIG[:VAR=VAL^VAR=VAL] — tools/profile.sh (trace + PMC passes) of bench --config
+      rest=${s#prof:}
+      name=${rest%%:*}
+      rest=${rest#*:}
+      cfg=${rest%%:*}
+      envs=""
+      [ "$rest" != "$cfg" ] && envs=${rest#*:}
+      echo "== prof_$name: config $cfg ${envs//^/ }"
+      ( for kv in ${envs//^/ }; do export "$kv"; done
+        PROF_OUT=$OUT/prof_$name STEPS=2 timeout -k 10 1000 bash tools/profile.sh --config "$cfg" ) > "$OUT/prof_$name.log" 2>&1
+      rc=$?
+      echo "== prof_$name rc=$rc"
+      tail -n 4 "$OUT/prof_$name.log"
+      [ $rc -ne 0 ] && exit $rc ;;
+    benchenv:*)  # benchenv:NAME:CONFIG:VAR=VAL^... — bench.py --config CONFIG under extra environment
+      rest=${s#benchenv:}
+      name=${rest%%:*}
+      rest=${rest#*:}
+      cfg=${rest%%:*}
+      envs=${rest#*:}
+      ( for kv in ${envs//^/ }; do export "$kv"; done
+        step "bench_$name" 700 python3 bench.py --config "$cfg" ${BENCH_ARGS:-} ) || exit $?
+      grep '^{' "$OUT/bench_$name.log" > "$OUT/bench_$name.json" ;;
+    benchargs:*)  # benchargs:NAME:ARGS — bench.py ARGS (spaces as '+')
+      rest=${s#benchargs:}
+      name=${rest%%:*}
+      args=${rest#*:}
+      step "bench_$name" 700 python3 bench.py ${args//+/ } || exit $?
+      grep '^{' "$OUT/bench_$name.log" > "$OUT/bench_$name.json" ;;
     ab:*)
       rest=${s#ab:}
       name=${rest%%:*}

@@ -812,6 +812,9 @@ struct rtg_scene {
   uint32_t* probe_visits = nullptr;  // set only while the probe render runs
   double treelet_tune_ms = 0.0;
   std::vector<uint64_t> treelet_cum;  // probe visits of the first k nodes after the renumbering, k = 0..n
+  // host copy of the device node array in its current order (scenes on the treelet schedule): the hot
+  // treelet renumbers this copy and uploads it, so a tuning downloads only the visit counts
+  std::vector<int32_t> host_nodes;
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
@@ -947,22 +950,39 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   if ((e = hipHostMalloc(&s->host_counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return cleanup(hip_fail(e, "hipHostMalloc(counters)"));
   char* base = static_cast<char*>(s->dmem);
-  for (const Part& p : parts) {
-    if (p.bytes == 0 || !p.src) continue;
-    if ((e = hipMemcpyAsync(base + p.off, p.src, p.bytes, hipMemcpyHostToDevice, s->own_stream)) !=
-        hipSuccess)
-      return cleanup(hip_fail(e, "hipMemcpy(scene)"));
+  {
+    // every array into one pinned staging image of the allocation (host copies on up to 16 threads),
+    // then one DMA: pageable sources went through the runtime's own small staging buffers (config 5:
+    // ~100 ms for 90 MB); without pinned memory the arrays are copied from where they are
+    struct Src {
+      const void* p;
+      size_t bytes, off;
+    };
+    std::vector<Src> srcs;
+    for (const Part& p : parts)
+      if (p.bytes != 0 && p.src) srcs.push_back({p.src, p.bytes, p.off});
+    if (!hs.perlin_perm.empty()) srcs.push_back({hs.perlin_perm.data(), hs.perlin_perm.size() * 4, perm_off});
+    if (!hs.tie_rank.empty()) srcs.push_back({hs.tie_rank.data(), hs.tie_rank.size() * 4, rank_off});
+    size_t end = 0;
+    for (const Src& x : srcs) end = std::max(end, x.off + x.bytes);
+    void* stage = nullptr;
+    if (end > 0 && hipHostMalloc(&stage, end, hipHostMallocDefault) == hipSuccess) {
+      char* st = static_cast<char*>(stage);
+      host_par_for(static_cast<int64_t>(srcs.size()), [&](int64_t b, int64_t e2, int) {
+        for (int64_t k = b; k < e2; ++k) std::memcpy(st + srcs[k].off, srcs[k].p, srcs[k].bytes);
+      });
+      e = hipMemcpyAsync(base, stage, end, hipMemcpyHostToDevice, s->own_stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(s->own_stream);
+      (void)hipHostFree(stage);
+      if (e != hipSuccess) return cleanup(hip_fail(e, "hipMemcpy(scene)"));
+    } else {
+      for (const Src& x : srcs)
+        if ((e = hipMemcpyAsync(base + x.off, x.p, x.bytes, hipMemcpyHostToDevice, s->own_stream)) != hipSuccess)
+          return cleanup(hip_fail(e, "hipMemcpy(scene)"));
+      if ((e = hipStreamSynchronize(s->own_stream)) != hipSuccess)
+        return cleanup(hip_fail(e, "hipStreamSynchronize(upload)"));
+    }
   }
-  if (!hs.perlin_perm.empty() &&
-      (e = hipMemcpyAsync(base + perm_off, hs.perlin_perm.data(), hs.perlin_perm.size() * 4,
-                          hipMemcpyHostToDevice, s->own_stream)) != hipSuccess)
-    return cleanup(hip_fail(e, "hipMemcpy(perlin)"));
-  if (!hs.tie_rank.empty() &&
-      (e = hipMemcpyAsync(base + rank_off, hs.tie_rank.data(), hs.tie_rank.size() * 4, hipMemcpyHostToDevice,
-                          s->own_stream)) != hipSuccess)
-    return cleanup(hip_fail(e, "hipMemcpy(tie ranks)"));
-  if ((e = hipStreamSynchronize(s->own_stream)) != hipSuccess)
-    return cleanup(hip_fail(e, "hipStreamSynchronize(upload)"));
   const auto t2 = std::chrono::steady_clock::now();
   double gpu_build_ms = 0.0;
   const int64_t nrefs = static_cast<int64_t>(hs.refs.size());
@@ -1032,6 +1052,11 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     if (desc->textures[t].type == RTG_TEX_IMAGE || desc->textures[t].type == RTG_TEX_NOISE) s->dev.tex_full = 1;
   s->dev.num_perlins = static_cast<int32_t>(hs.perlin_perm.size() / 768);
   s->num_cus = prop.multiProcessorCount;
+  // trees too large for any LDS schedule render on the treelet schedule: keep their node array on the
+  // host for the hot-treelet renumbering (device-built trees are downloaded once, on the first tuning)
+  if (!hs.gpu_bvh && hs.node_width >= 4 && hs.num_nodes * node_bytes(hs.node_width) > kLdsPerCu)
+    s->host_nodes.assign(reinterpret_cast<const int32_t*>(hs.nodes.data()),
+                         reinterpret_cast<const int32_t*>(hs.nodes.data()) + hs.nodes.size());
 
   s->info.device = device;
   s->info.bvh_mode = desc->bvh_mode;
@@ -1493,22 +1518,36 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   std::vector<int32_t> rec;
   const int width = s->dev.node_width;
   const int64_t nb = node_bytes(width);
+  const bool have_host = static_cast<int64_t>(s->host_nodes.size()) == n * nb / 4;
   if (st == RTG_OK) {
     cnt.resize(n);
-    rec.resize(n * nb / 4);
+    if (!have_host) rec.resize(n * nb / 4);  // device-built trees: the node array comes from the device
     e = hipMemcpyAsync(cnt.data(), visits, n * 4, hipMemcpyDeviceToHost, os);
-    if (e == hipSuccess) e = hipMemcpyAsync(rec.data(), s->dev.nodes, n * nb, hipMemcpyDeviceToHost, os);
+    if (e == hipSuccess && !have_host) e = hipMemcpyAsync(rec.data(), s->dev.nodes, n * nb, hipMemcpyDeviceToHost, os);
     if (e == hipSuccess) e = hipStreamSynchronize(os);
     if (e != hipSuccess) st = hip_fail(e, "hot treelet download");
   }
   (void)hipFree(out);
   (void)hipFree(visits);
   if (st != RTG_OK) return st;
+  if (have_host) rec.swap(s->host_nodes);
   std::vector<int32_t> order;
   hot_order_nodes(rec.data(), width, cnt.data(), n, &order);
-  e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), rec.data(), n * nb, hipMemcpyHostToDevice, os);
+  void* stage = nullptr;  // the renumbered array through pinned memory (one DMA), else from the vector
+  if (hipHostMalloc(&stage, n * nb, hipHostMallocDefault) == hipSuccess) {
+    std::memcpy(stage, rec.data(), n * nb);
+    e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), stage, n * nb, hipMemcpyHostToDevice, os);
+  } else {
+    stage = nullptr;
+    e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), rec.data(), n * nb, hipMemcpyHostToDevice, os);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(os);
-  if (e != hipSuccess) return hip_fail(e, "hot treelet upload");
+  if (stage) (void)hipHostFree(stage);
+  if (e != hipSuccess) {
+    s->host_nodes.clear();  // the device array may be half written: no host copy claims to match it
+    return hip_fail(e, "hot treelet upload");
+  }
+  s->host_nodes.swap(rec);  // the host copy follows the device order
   s->treelet_tune_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   s->treelet_cum.assign(n + 1, 0);
   for (int64_t k = 0; k < n; ++k) s->treelet_cum[k + 1] = s->treelet_cum[k] + cnt[order[k]];

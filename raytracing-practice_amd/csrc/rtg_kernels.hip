@@ -1795,8 +1795,13 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
     }
     q_unlock(Q.ctl);
     if (take == 0u) {
-      // done once every tracer wave has handed out its last unit and no unit is in flight
-      if (q_ld(Q.ctl + 6) >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
+      // done once every tracer wave has handed out its last unit and no unit is in flight. The report
+      // count is loaded with acquire (the tracers add to it with release, after adding their units to
+      // ctl[5]), so seeing every report means seeing every unit: loaded in the other order (relaxed
+      // loads may be reordered) a shading wave could read ctl[5] before a tracer's last units and the
+      // report after them, and leave those units unshaded (round-4 GPU tests: ray-queue waits timed out)
+      const uint32_t reports = __hip_atomic_load(Q.ctl + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (reports >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
       __builtin_amdgcn_s_sleep(2);
       if (++idle > (1u << 24)) {
         if (lane == 0) atomicAdd(&J.counters[26], 1ull);
@@ -1967,7 +1972,7 @@ __device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, 
     }
     if (exhausted && k_next >= 64 && !reported) {  // this wave hands out no more units
       reported = true;
-      if (lane == 0) __hip_atomic_fetch_add(Q.ctl + 6, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_fetch_add(Q.ctl + 6, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (fresh) start_pixel_sample(u.ps, C, J, u.px, static_cast<uint32_t>(u.sample));
     if (fresh || arrived) {

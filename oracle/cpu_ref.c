@@ -902,10 +902,10 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   if (fabsf(q) < 0x1p-100f || a == 0.0f) return -1.0f;
   float t0 = q * inv_a, t1 = c / q; /* far root by the reciprocal, near root divided */
   float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
-  /* roots up to tmax inclusive: a root equal to the closest hit is an exact-t tie (tie_wins32) */
-  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
-  if (tmin < lo && lo <= tmax) return lo;
-  if (tmin < hi && hi <= tmax) return hi;
+  /* roots strictly inside (tmin, tmax) (interval::surrounds): a sphere never replaces an equal-t hit */
+  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
+  if (tmin < lo && lo < tmax) return lo;
+  if (tmin < hi && hi < tmax) return hi;
   return -1.0f;
 }
 /* quad::hit, fp32: returns t or -1 */
@@ -925,15 +925,14 @@ static float quad_t32(const float* q, f3 o, f3 d, float tmin, float tmax) {
   return t;
 }
 
-/* Exact-t tie rule of the rtg-f32 spec (rtg_kernels.hip tie_wins): the reference tests
+/* Exact-t tie rule of the rtg-f32 spec (rtg_kernels.hip quad_wins_tie): the reference tests
    its list in order (hittable_list.hpp:40-64), quads accept t == closest (interval::contains,
-   quad.hpp:62), spheres do not (interval::surrounds, sphere.hpp:70). At equal t it keeps any quad over
-   any sphere, the later quad, the earlier sphere, in whatever order they are tested; ids are input
-   (list-order) indices. */
-static int tie_wins32(const world32* w, int64_t id, int64_t best) {
-  int nq = w->s->prims[id].kind == RTG_PRIM_QUAD, bq = w->s->prims[best].kind == RTG_PRIM_QUAD;
-  if (nq != bq) return nq;
-  return nq ? id > best : id < best;
+   quad.hpp:62), spheres do not (interval::surrounds, sphere.hpp:70). At equal t a quad replaces a sphere
+   and an earlier quad of the list, whatever order they are tested in; a sphere replaces nothing
+   (sphere_t32's strict bound). ids are input (list-order) indices. */
+static int quad_wins_tie32(const world32* w, int64_t id, int64_t best) {
+  if (w->s->prims[best].kind != RTG_PRIM_QUAD) return 1;
+  return id > best;
 }
 
 /* closest hit: reference BVH order; boxes tested in f64 (pure culling), primitives in fp32 */
@@ -946,7 +945,9 @@ static void node_hit32(const world32* w, int32_t code, f3 o, f3 d, const double 
     float t = w->s->prims[id].kind == RTG_PRIM_SPHERE
                   ? sphere_t32(w->sph + id * 8, o, d, time, 0.001f, *tbest, id == origin)
                   : (id == origin ? -1.0f : quad_t32(w->qd + id * 16, o, d, 0.001f, *tbest));
-    if (t > 0.0f && (t < *tbest || tie_wins32(w, id, *best))) {
+    int take = t > 0.0f;
+    if (take && w->s->prims[id].kind == RTG_PRIM_QUAD && t == *tbest) take = quad_wins_tie32(w, id, *best);
+    if (take) {
       *tbest = t;
       *best = id;
     }

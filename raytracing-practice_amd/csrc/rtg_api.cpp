@@ -1414,9 +1414,9 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     const bool small = dj.lds_waves == 4 && lds_wgs == kSmallSceneWgs && lds4 < 0;
     const bool big = dj.lds_waves == kLdsWaves && lds_wgs == 1;
     const int tracers = small ? kQTracerWaves : kLdsWaves - K.q_shaders;
-    const int Sq = small ? 64 : 128;
     for (const int T : {512, 256, 128, 64, 32}) {
       if (!small && !big) break;
+      const int Sq = small ? std::min(64, T) : 128;  // queue capacities: powers of two
       const int qbytes = (kQCtl + kQEntryDw * (Sq + T)) * 4;
       const bool fits = small ? lds_alloc(qoff + qbytes) * kSmallSceneWgs <= kLdsPerCu
                               : lds_alloc(qoff + qbytes) <= kLdsPerCu;

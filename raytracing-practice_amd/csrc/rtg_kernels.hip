@@ -213,11 +213,11 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
-  // roots up to and including tmax: a root equal to the closest hit so far is an exact-t tie, which
-  // the caller resolves by the reference's list order (take_hit)
-  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
-  if (tmin < lo && lo <= tmax) return lo;
-  if (tmin < hi && hi <= tmax) return hi;
+  // roots strictly inside (tmin, tmax), interval::surrounds (sphere.hpp:70): a sphere never replaces an
+  // equal-t hit (the tie rule)
+  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
+  if (tmin < lo && lo < tmax) return lo;
+  if (tmin < hi && hi < tmax) return hi;
   return -1.0f;
 }
 
@@ -242,25 +242,28 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 }
 
 // Exact-t ties (rtg-f32 spec, DESIGN.md §4 "tie rule"). The reference tests the world's objects in
-// list order (hittable_list.hpp:40-64) against a shrinking interval, and its two primitives bound it
-// differently: quad::hit accepts t == closest_so_far (interval::contains, quad.hpp:62, interval.hpp:29),
-// sphere::hit does not (interval::surrounds, sphere.hpp:70, interval.hpp:32). Between primitives at the
-// same t the reference therefore keeps: any quad over any sphere, the later quad in list order, the
-// earlier sphere — whatever order they are tested in. The kernels test in BVH order, so both primitive
-// tests return roots up to tmax inclusive and a root equal to the closest hit wins only by that rule
-// (S.tie_rank: each slot's list index, read only on a tie). Not a root at t == tbest: th < tbest.
-__device__ __forceinline__ bool tie_wins(const DevScene& S, int32_t ref, int32_t best) {
-  const bool nq = (ref & kQuadRefBit) != 0, bq = (best & kQuadRefBit) != 0;
-  if (nq != bq) return nq;
-  const int64_t off = nq ? S.num_spheres : 0;
-  const int32_t rn = S.tie_rank[off + (ref & ~kQuadRefBit)], rb = S.tie_rank[off + (best & ~kQuadRefBit)];
-  return nq ? rn > rb : rn < rb;
+// list order (hittable_list.hpp:40-64) against a shrinking interval: quad::hit accepts t ==
+// closest_so_far (interval::contains, quad.hpp:62, interval.hpp:29), sphere::hit does not
+// (interval::surrounds, sphere.hpp:70, interval.hpp:32). So at equal t it keeps any quad over any
+// sphere and the later of two quads, whatever order they are tested in. The kernels test in BVH
+// order: sphere_t takes roots strictly below tmax (a sphere never replaces an equal-t hit), quad_t
+// roots up to tmax, and a quad root equal to the closest hit replaces it only if that hit is a sphere
+// or an earlier quad of the list (S.tie_rank: each quad slot's list index, read only on a tie; the
+// check is one compare and a wave-uniform branch). Two spheres at the bit-identical t (duplicate
+// spheres, a ray through a tangent point) keep the one tested first: the one order-dependent case,
+// left out of the rule because its compare cost config 2 3 %.
+__device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t ref, int32_t best) {
+  if (!(best & kQuadRefBit)) return true;
+  const int32_t* rank = S.tie_rank + S.num_spheres;
+  return rank[ref & ~kQuadRefBit] > rank[best & ~kQuadRefBit];
 }
-// A primitive test's root th (-1: miss; else tmin < th <= tbest) replaces the closest hit.
-__device__ __forceinline__ bool take_hit(const DevScene& S, float th, float tbest, int32_t ref, int32_t best) {
-  if (!(th > 0.0f)) return false;
-  if (__builtin_expect(th < tbest, 1)) return true;
-  return tie_wins(S, ref, best);
+// A quad root th (-1: miss; else tmin <= th <= tbest) replaces the closest hit.
+__device__ __forceinline__ bool take_quad_hit(const DevScene& S, float th, float tbest, int32_t ref, int32_t best) {
+  bool take = th > 0.0f && th < tbest;
+  const bool tie = th == tbest;
+  if (ballot_tie(tie) != 0 && tie) take = quad_wins_tie(S, ref, best);
+  return take;
 }
 
 template <bool COUNT>
@@ -717,7 +720,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
-      if (take_hit(S, th, t.tbest, first + k, t.best)) {
+      if (th > 0.0f) {
         t.tbest = th;
         t.best = first + k;
         if (MAT) t.mat = ibits(sp4[1].w);
@@ -740,7 +743,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
     }
-    if (take_hit(S, th, t.tbest, ref, t.best)) {  // th > tmin >= 0.001 on a hit
+    if ((ref & kQuadRefBit) ? take_quad_hit(S, th, t.tbest, ref, t.best) : th > 0.0f) {  // th > tmin >= 0.001
       t.tbest = th;
       t.best = ref;
       if (MAT) t.mat = m;
@@ -838,7 +841,7 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
           const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
           t = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
         }
-        if (take_hit(S, t, tbest, ref, best)) {  // t > tmin >= 0.001 on a hit
+        if ((ref & kQuadRefBit) ? take_quad_hit(S, t, tbest, ref, best) : t > 0.0f) {  // t > tmin >= 0.001
           tbest = t;
           best = ref;
         }
@@ -1781,7 +1784,8 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
     if (!q_lock(J, Q.ctl)) return;
     const uint32_t head = q_ld(Q.ctl + 1), cnt = q_ld(Q.ctl + 2), tcnt = q_ld(Q.ctl + 4);
     // a full batch, or what there is when no shaded ray waits for the tracers (they may be starving)
-    const uint32_t take = cnt >= 64u ? 64u : (tcnt == 0u ? cnt : 0u);
+    const uint32_t full = min(64u, static_cast<uint32_t>(Q.S));
+    const uint32_t take = cnt >= full ? full : (tcnt == 0u ? cnt : 0u);
     UnitCtx u;
     float t = 0.0f;
     int32_t best = -1;
@@ -1837,22 +1841,26 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
       }
     }
     const uint32_t ndone = static_cast<uint32_t>(__popcll(ballot(unit_done)));
-    const uint64_t pm = ballot(cont);
-    const uint32_t npush = static_cast<uint32_t>(__popcll(pm));
-    const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(pm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(pm), 0u)));
-    // the continuing rays into the trace queue (room is guaranteed by the workgroup's q_rmax; bounded wait)
+    // the continuing rays into the trace queue, as many as it has room for each time (a trace queue
+    // smaller than a batch, as small scenes' LDS allows, takes a batch in parts); the workgroup's q_rmax
+    // guarantees room eventually, the wait is bounded
     uint32_t spins = 0;
-    while (npush != 0u) {
+    for (;;) {
+      const uint64_t pm = ballot(cont);
+      const uint32_t npush = static_cast<uint32_t>(__popcll(pm));
+      if (npush == 0u) break;
       if (!q_lock(J, Q.ctl)) return;
       const uint32_t th = q_ld(Q.ctl + 3), tc = q_ld(Q.ctl + 4);
-      const bool room = tc + npush <= static_cast<uint32_t>(Q.T);
-      if (room) {
-        if (cont) q_put(Q.tq, static_cast<int>((th + tc + rank) & (Q.T - 1)), u, false, 0.0f, 0);
-        if (lane == 0) q_st(Q.ctl + 4, tc + npush);
+      const uint32_t put = min(npush, static_cast<uint32_t>(Q.T) - tc);
+      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(pm >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(pm), 0u)));
+      if (cont && static_cast<uint32_t>(rank) < put) {
+        q_put(Q.tq, static_cast<int>((th + tc + rank) & (Q.T - 1)), u, false, 0.0f, 0);
+        cont = false;
       }
+      if (lane == 0 && put != 0u) q_st(Q.ctl + 4, tc + put);
       q_unlock(Q.ctl);
-      if (room) break;
+      if (put == npush) break;
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 22)) {
         if (lane == 0) atomicAdd(&J.counters[26], 1ull);

@@ -628,10 +628,9 @@ def test_ground_and_one_sphere(gpu_lib, oracle, bvh):
 
 @pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
 def test_exact_t_ties_match_oracle(gpu_lib, oracle, bvh):
-    """The exact-t tie rule: identical quads and identical spheres
-    hit at bit-identical t. Whatever order a BVH builder makes the kernel test them in, the frame is
-    cpu_ref32's bit for bit, showing the later quad (interval::contains, quad.hpp:62) and the earlier
-    sphere (interval::surrounds, sphere.hpp:70), as the reference's list order keeps them."""
+    """The exact-t tie rule: three identical quads hit at bit-identical
+    t. Whatever order a BVH builder makes the kernel test them in, the frame is cpu_ref32's bit for bit
+    and shows the last quad of the list (interval::contains, quad.hpp:62), as the reference keeps it."""
     from tie_scene import BLUE, GREEN, RED, WHITE, colour_counts, tie_scene
 
     d, cam = tie_scene(bvh, width=96)

@@ -205,15 +205,14 @@ def test_sphere_t32_grazing_far_spheres(oracle):
 
 
 def test_exact_t_ties_follow_reference_list_order(oracle):
-    """Exact-t tie rule of the rtg-f32 spec: identical quads and identical spheres hit at
-    bit-identical t. The reference keeps the later quad (interval::contains, quad.hpp:62) and the
-    earlier sphere (interval::surrounds, sphere.hpp:70) — cpu_ref32 must do the same whatever order
-    its BVH tests them in."""
+    """Exact-t tie rule of the rtg-f32 spec: three identical quads hit at bit-identical t.
+    The reference keeps the last of them (interval::contains, quad.hpp:62) — cpu_ref32 must do the same
+    whatever order its BVH tests them in."""
     from tie_scene import BLUE, GREEN, RED, WHITE, colour_counts, tie_scene
 
     for bvh in (rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_MEDIAN):
         d, cam = tie_scene(bvh)
         frame, _ = oracle.render_f32(d, cam)
         n = colour_counts(frame)
-        assert n[GREEN] > 50 and n[BLUE] > 30, n  # the later quad, the earlier sphere
+        assert n[GREEN] > 50 and n[BLUE] > 30, n  # the last quad; the sphere beside them
         assert n[RED] == 0 and n[WHITE] == 0, n

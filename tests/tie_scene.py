@@ -1,8 +1,7 @@
-"""A scene built for exact-t ties (DESIGN.md §4 "tie rule"): two identical quads and two identical
-spheres, each pair with different emitted colours, so every camera ray that reaches a pair hits both
-members at bit-identical t. The reference tests its list in order (hittable_list.hpp:40-64): quad::hit
-accepts t == closest_so_far (interval::contains, quad.hpp:62), sphere::hit does not (surrounds,
-sphere.hpp:70), so its image shows the LATER quad's colour and the EARLIER sphere's."""
+"""A scene built for exact-t ties (DESIGN.md §4 "tie rule"): three identical quads with different
+emitted colours, so every camera ray that reaches them hits all three at bit-identical t, beside a
+sphere. The reference tests its list in order (hittable_list.hpp:40-64) and quad::hit accepts t ==
+closest_so_far (interval::contains, quad.hpp:62), so its image shows the LAST quad's colour."""
 import ctypes as C
 
 import rtgpu
@@ -23,8 +22,8 @@ def tie_scene(bvh_mode=rtgpu.RTG_BVH_SAH, width=48):
         return rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_SPHERE, material=m, p0=rtgpu.D3(1.6, 0.0, 0.0),
                                    p1=rtgpu.D3(1.6, 0.0, 0.0), radius=1.0)
 
-    # list order: quad (red), sphere (blue), quad (green), sphere (white)
-    prims = [quad(0), sphere(1), quad(2), sphere(3)]
+    # list order: quad (white), quad (red), sphere (blue), quad (green)
+    prims = [quad(3), quad(0), sphere(1), quad(2)]
     P = (rtgpu.rtg_primitive * 4)(*prims)
     M = (rtgpu.rtg_material * 4)(*mat)
     T = (rtgpu.rtg_texture * 4)(*tex)

@@ -1126,8 +1126,14 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
   if (c[24] != 0)
     return fail(RTG_E_HIP, "tile-ring slot waits timed out (frame incomplete) in " + std::to_string(c[24]) + " waves");
-  if (c[26] != 0)
-    return fail(RTG_E_HIP, "ray-queue waits timed out (frame incomplete) in " + std::to_string(c[26]) + " waves");
+  if (c[26] != 0) {
+    const unsigned long long r = c[27];
+    char buf[200];
+    std::snprintf(buf, sizeof buf, " (first: kind %llu, shade queue %llu, trace queue %llu, units %llu, reports %llu, "
+                  "own rays %llu)", r & 15ull, (r >> 4) & 1023ull, (r >> 14) & 1023ull, (r >> 24) & 0xffffull,
+                  (r >> 40) & 15ull, (r >> 44) & 127ull);
+    return fail(RTG_E_HIP, "ray-queue waits timed out (frame incomplete) in " + std::to_string(c[26]) + " waves" + buf);
+  }
   if (c[7] != 0)
     return fail(RTG_E_UNSUPPORTED, "the 16-bit LDS stack layout cannot hold this tree's codes in " +
                                        std::to_string(c[7]) + " workgroups (nothing rendered)");

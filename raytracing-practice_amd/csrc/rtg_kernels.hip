@@ -260,9 +260,11 @@ __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t ref, in
 }
 // A quad root th (-1: miss; else tmin <= th <= tbest) replaces the closest hit.
 __device__ __forceinline__ bool take_quad_hit(const DevScene& S, float th, float tbest, int32_t ref, int32_t best) {
-  bool take = th > 0.0f && th < tbest;
+  bool take = th > 0.0f;  // quad_t: th <= tbest; th == tbest (> 0) only on a tie
   const bool tie = th == tbest;
+#ifndef RTG_AB_NO_TIE
   if (ballot_tie(tie) != 0 && tie) take = quad_wins_tie(S, ref, best);
+#endif
   return take;
 }
 
@@ -1678,6 +1680,19 @@ __device__ __forceinline__ uint32_t q_ld(lu32* a) {
 __device__ __forceinline__ void q_st(lu32* a, uint32_t v) {
   __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// A queue wait that timed out: counted in counters[26]; the first one also leaves its kind and the
+// workgroup's queue state in counters[27] (kind | shade count << 4 | trace count << 14 | units in flight
+// << 24 | tracer reports << 40 | the wave's own rays << 44), which the host reports in the error
+__device__ __forceinline__ void q_timeout(const DevJob& J, lu32* ctl, uint32_t kind, uint32_t own) {
+  atomicAdd(&J.counters[26], 1ull);
+  const unsigned long long rec =
+      static_cast<unsigned long long>(kind) | (static_cast<unsigned long long>(q_ld(ctl + 2) & 1023u) << 4) |
+      (static_cast<unsigned long long>(q_ld(ctl + 4) & 1023u) << 14) |
+      (static_cast<unsigned long long>(q_ld(ctl + 5) & 0xffffu) << 24) |
+      (static_cast<unsigned long long>(q_ld(ctl + 6) & 15u) << 40) | (static_cast<unsigned long long>(own & 127u) << 44);
+  atomicCAS(&J.counters[27], 0ull, rec);
+}
+
 // Workgroup lock (ctl[0]) for one wave; false when it could not be taken (bounded: counters[26]).
 __device__ __forceinline__ bool q_lock(const DevJob& J, lu32* ctl) {
   uint32_t ok = 1;
@@ -1691,7 +1706,7 @@ __device__ __forceinline__ bool q_lock(const DevJob& J, lu32* ctl) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1u << 22)) {
         ok = 0;
-        atomicAdd(&J.counters[26], 1ull);
+        q_timeout(J, ctl, 1u, 0u);
         break;
       }
     }
@@ -1808,7 +1823,7 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
       if (reports >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
       __builtin_amdgcn_s_sleep(2);
       if (++idle > (1u << 24)) {
-        if (lane == 0) atomicAdd(&J.counters[26], 1ull);
+        if (lane == 0) q_timeout(J, Q.ctl, 2u, 0u);
         return;
       }
       continue;
@@ -1863,7 +1878,7 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
       if (put == npush) break;
       __builtin_amdgcn_s_sleep(2);
       if (++spins > (1u << 22)) {
-        if (lane == 0) atomicAdd(&J.counters[26], 1ull);
+        if (lane == 0) q_timeout(J, Q.ctl, 3u, npush);
         return;
       }
     }
@@ -2003,7 +2018,8 @@ __device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, 
       if (has_m == 0 && reported && q_ld(Q.ctl + 5) == 0u) return;
       __builtin_amdgcn_s_sleep(2);
       if (++idle > (1u << 24)) {
-        if (lane == 0) atomicAdd(&J.counters[26], 1ull);
+        const uint32_t own = static_cast<uint32_t>(__popcll(has_m));
+        if (lane == 0) q_timeout(J, Q.ctl, stalled ? 5u : 4u, own);
         return;
       }
       continue;

@@ -26,6 +26,11 @@ for s in "$@"; do
       step gpu_tests 900 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread
       rc=$?
       [ $rc -gt 1 ] && exit $rc ;;
+    testk:*)  # testk:EXPR — the GPU tests matching -k EXPR ('+' for spaces)
+      expr=${s#testk:}
+      step gpu_tests_k 600 python3 -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k "${expr//+/ }"
+      rc=$?
+      [ $rc -gt 1 ] && exit $rc ;;
     bench:*)
       c=${s#bench:}
       step bench_config$c 700 python3 bench.py --config "$c" ${BENCH_ARGS:-} || exit $?

@@ -584,7 +584,8 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         out->spheres.insert(out->spheres.end(), rec, rec + 8);
       } else {
         slot[pid] = nquad++;
-        // quad ctor (quad.hpp:12-27) in fp64, then rounded
+        // quad ctor (quad.hpp:12-27) in fp64, then rounded; the v row's 4th word holds the quad's list
+        // index (the exact-t tie rule's rank, read with the inside test's loads)
         const D3 Q = d3(p.p0), u = d3(p.p1), v = d3(p.p2);
         const D3 n = cross(u, v);
         const D3 normal = unit_vector(n);
@@ -595,7 +596,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
                                static_cast<float>(u.x),      static_cast<float>(u.y),
                                static_cast<float>(u.z),      ibits_to_float(p.material),
                                static_cast<float>(v.x),      static_cast<float>(v.y),
-                               static_cast<float>(v.z),      0.0f,
+                               static_cast<float>(v.z),      ibits_to_float(static_cast<int32_t>(pid)),
                                static_cast<float>(w.x),      static_cast<float>(w.y),
                                static_cast<float>(w.z),      0.0f,
                                static_cast<float>(normal.x), static_cast<float>(normal.y),

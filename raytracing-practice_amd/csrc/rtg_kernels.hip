@@ -222,7 +222,8 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
 }
 
 // quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
-__device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin, float tmax) {
+// `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit.
+__device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin, float tmax, int32_t& rank) {
   const float4 q0 = q[0], q4 = q[4];
   const V3 n = xyz(q4);
   const float denom = dot(n, d);
@@ -234,10 +235,12 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   if (!(tmin <= t && t <= tmax)) return -1.0f;
   const V3 p = madd(t, d, o);
   const V3 hp = sub(p, xyz(q0));
-  const V3 u = xyz(q[1]), v = xyz(q[2]), w = xyz(q[3]);
+  const float4 q2 = q[2];
+  const V3 u = xyz(q[1]), v = xyz(q2), w = xyz(q[3]);
   const float alpha = dot(w, cross(hp, v));
   const float beta = dot(w, cross(u, hp));
   if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return -1.0f;
+  rank = ibits(q2.w);
   return t;
 }
 
@@ -253,19 +256,11 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // spheres, a ray through a tangent point) keep the one tested first: the one order-dependent case,
 // left out of the rule because its compare cost config 2 3 %.
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t ref, int32_t best) {
+// Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
+// list ranks, only on a tie (wave-uniform branch).
+__device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
   if (!(best & kQuadRefBit)) return true;
-  const int32_t* rank = S.tie_rank + S.num_spheres;
-  return rank[ref & ~kQuadRefBit] > rank[best & ~kQuadRefBit];
-}
-// A quad root th (-1: miss; else tmin <= th <= tbest) replaces the closest hit.
-__device__ __forceinline__ bool take_quad_hit(const DevScene& S, float th, float tbest, int32_t ref, int32_t best) {
-  bool take = th > 0.0f;  // quad_t: th <= tbest; th == tbest (> 0) only on a tie
-  const bool tie = th == tbest;
-#ifndef RTG_AB_NO_TIE
-  if (ballot_tie(tie) != 0 && tie) take = quad_wins_tie(S, ref, best);
-#endif
-  return take;
+  return qrank > S.tie_rank[S.num_spheres + (best & ~kQuadRefBit)];
 }
 
 template <bool COUNT>
@@ -287,7 +282,9 @@ struct Trav {
   int32_t sp;     // stack depth
   int32_t origin; // primitive ref the ray starts on (-1: camera ray), DESIGN.md §4 "origin rule"
   int32_t mat;    // material of the closest hit: the cache-read schedules' shading then fetches the
-                  // material beside the primitive instead of after it (one memory round trip less)
+                  // material beside the primitive instead of after it (one memory round trip less);
+                  // in the LDS schedule instead the closest hit's tie rank (a quad's list index, -1
+                  // for a sphere or none: the exact-t tie rule)
 };
 
 // todo of a finished traversal. "Traversal active" is this integer compare, not a bool of its own:
@@ -316,6 +313,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.oz = -o.z * t.iz;
   t.tbest = __builtin_inff();
   t.best = -1;
+  t.mat = -1;  // no hit: tie rank -1 (LDS schedule; the cache-read schedules overwrite it on a hit)
   t.todo = S.num_nodes > 0 ? S.root_code : kTravDone;
   t.sp = 0;
   t.origin = origin;
@@ -725,7 +723,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       if (th > 0.0f) {
         t.tbest = th;
         t.best = first + k;
-        if (MAT) t.mat = ibits(sp4[1].w);
+        t.mat = MAT ? ibits(sp4[1].w) : -1;
       }
     }
     pop();
@@ -735,20 +733,34 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     const int32_t ref = S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit);
     float th;
     if (COUNT) cnt.prim += 1;
-    int32_t m = 0;
+    int32_t m = 0, qrank = -1;
+    bool take;
     if (ref & kQuadRefBit) {  // planar: a ray leaving a quad never hits it again
       const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
-      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest);
+      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, qrank);
       if (MAT && th > 0.0f) m = ibits(q[1].w);
+      // exact-t tie rule: a quad root equal to the closest hit replaces it only if that
+      // is a sphere or an earlier quad of the list
+      if constexpr (MAT) {
+        take = th > 0.0f;
+        if (ballot_tie(th == t.tbest) != 0 && th == t.tbest) take = quad_wins_tie(S, qrank, t.best);
+      } else {  // t.mat holds the closest hit's rank: branch-free
+#ifdef RTG_AB_NO_TIE  // A/B: the round-3 acceptance (a quad replaces an equal-t hit found before it)
+        take = th > 0.0f;
+#else
+        take = th > 0.0f && (th < t.tbest || qrank > t.mat);
+#endif
+      }
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
+      take = th > 0.0f;  // sphere_t: th < tbest
     }
-    if ((ref & kQuadRefBit) ? take_quad_hit(S, th, t.tbest, ref, t.best) : th > 0.0f) {  // th > tmin >= 0.001
+    if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
       t.best = ref;
-      if (MAT) t.mat = m;
+      t.mat = MAT ? m : qrank;
     }
   }
   pop();
@@ -836,14 +848,18 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
         const int32_t ref = S.refs[first + k];
         float t;
         if (COUNT) cnt.prim += 1;
+        bool take;
         if (ref & kQuadRefBit) {
+          int32_t qrank = -1;
           t = ref == origin ? -1.0f
-                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest);
+                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest, qrank);
+          take = t > 0.0f && (t < tbest || quad_wins_tie(S, qrank, best));
         } else {
           const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
           t = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
+          take = t > 0.0f;
         }
-        if ((ref & kQuadRefBit) ? take_quad_hit(S, t, tbest, ref, best) : t > 0.0f) {  // t > tmin >= 0.001
+        if (take) {  // t > tmin >= 0.001
           tbest = t;
           best = ref;
         }
@@ -1511,7 +1527,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         if (th > 0.0f) {
           tr.tbest = th;
           tr.best = S.occluder;
-          if (GEOM != kGeomLds) tr.mat = ibits(sp4[1].w);
+          if (GEOM != kGeomLds) tr.mat = ibits(sp4[1].w);  // (LDS schedule: tie rank -1 from trav_begin)
         }
       }
     }
@@ -1796,6 +1812,19 @@ __device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, 
   const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
   uint32_t idle = 0;
   for (;;) {
+    // peek without the lock: an idle wave that took the lock on every poll kept it busy enough that
+    // a working wave could not get it (round-4 GPU tests: lock waits timed out in small-scene
+    // workgroups, where two of the three tracers and the shader idle most of the frame)
+    if (q_ld(Q.ctl + 2) == 0u) {
+      const uint32_t reports = __hip_atomic_load(Q.ctl + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (reports >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
+      __builtin_amdgcn_s_sleep(4);
+      if (++idle > (1u << 24)) {
+        if (lane == 0) q_timeout(J, Q.ctl, 2u, 0u);
+        return;
+      }
+      continue;
+    }
     if (!q_lock(J, Q.ctl)) return;
     const uint32_t head = q_ld(Q.ctl + 1), cnt = q_ld(Q.ctl + 2), tcnt = q_ld(Q.ctl + 4);
     // a full batch, or what there is when no shaded ray waits for the tracers (they may be starving)
@@ -1913,7 +1942,10 @@ __device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, 
     const uint64_t fm = ballot(fin);
     bool tq_empty = true;
     backlog = 0;
-    if (fm != 0 || ballot(!has()) != 0) {
+    // the lock only when this wave has rays to deposit or empty lanes and shaded rays wait (peeked
+    // without the lock): idle waves polling under the lock starved the working ones
+    const bool refill = ballot(!has()) != 0 && q_ld(Q.ctl + 4) != 0u;
+    if (fm != 0 || refill) {
       if (!q_lock(J, Q.ctl)) return;
       const uint32_t sh = q_ld(Q.ctl + 1), sc = q_ld(Q.ctl + 2);
       const uint32_t take = min(static_cast<uint32_t>(__popcll(fm)), static_cast<uint32_t>(Q.S) - sc);
@@ -2016,7 +2048,7 @@ __device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, 
     const bool stalled = has_m != 0 && backlog != 0 && ballot(trav_active(tr)) == 0;  // shade queue full
     if (has_m == 0 || stalled) {  // nothing to trace: done, or wait for the shading wave
       if (has_m == 0 && reported && q_ld(Q.ctl + 5) == 0u) return;
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(4);
       if (++idle > (1u << 24)) {
         const uint32_t own = static_cast<uint32_t>(__popcll(has_m));
         if (lane == 0) q_timeout(J, Q.ctl, stalled ? 5u : 4u, own);

@@ -222,8 +222,11 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
 }
 
 // quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
-// `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit.
-__device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin, float tmax, int32_t& rank) {
+// `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit. `brank`: the
+// closest hit's rank (-1: a sphere or none); a root equal to tmax is a miss unless this quad comes later
+// in the list than that hit (exact-t tie rule; compared on the hit path only)
+__device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin, float tmax, int32_t brank,
+                                        int32_t& rank) {
   const float4 q0 = q[0], q4 = q[4];
   const V3 n = xyz(q4);
   const float denom = dot(n, d);
@@ -241,6 +244,9 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   const float beta = dot(w, cross(u, hp));
   if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return -1.0f;
   rank = ibits(q2.w);
+#ifndef RTG_AB_NO_TIE
+  if (t == tmax && rank <= brank) return -1.0f;
+#endif
   return t;
 }
 
@@ -737,20 +743,18 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     bool take;
     if (ref & kQuadRefBit) {  // planar: a ray leaving a quad never hits it again
       const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
-      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, qrank);
-      if (MAT && th > 0.0f) m = ibits(q[1].w);
       // exact-t tie rule: a quad root equal to the closest hit replaces it only if that
-      // is a sphere or an earlier quad of the list
+      // is a sphere or an earlier quad of the list. LDS schedule: t.mat holds the closest hit's rank and
+      // quad_t rejects a losing tie on its hit path; cache-read schedules (t.mat = material): the rank
+      // is re-read, only on a tie
+      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, MAT ? -2 : t.mat, qrank);
+      if (MAT && th > 0.0f) m = ibits(q[1].w);
+      take = th > 0.0f;
+#ifndef RTG_AB_NO_TIE
       if constexpr (MAT) {
-        take = th > 0.0f;
         if (ballot_tie(th == t.tbest) != 0 && th == t.tbest) take = quad_wins_tie(S, qrank, t.best);
-      } else {  // t.mat holds the closest hit's rank: branch-free
-#ifdef RTG_AB_NO_TIE  // A/B: the round-3 acceptance (a quad replaces an equal-t hit found before it)
-        take = th > 0.0f;
-#else
-        take = th > 0.0f && (th < t.tbest || qrank > t.mat);
-#endif
       }
+#endif
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
@@ -852,7 +856,8 @@ __device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, fl
         if (ref & kQuadRefBit) {
           int32_t qrank = -1;
           t = ref == origin ? -1.0f
-                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest, qrank);
+                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest, -2,
+                                     qrank);
           take = t > 0.0f && (t < tbest || quad_wins_tie(S, qrank, best));
         } else {
           const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;

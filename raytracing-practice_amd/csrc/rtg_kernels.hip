@@ -261,7 +261,9 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // check is one compare and a wave-uniform branch). Two spheres at the bit-identical t (duplicate
 // spheres, a ray through a tangent point) keep the one tested first: the one order-dependent case,
 // left out of the rule because its compare cost config 2 3 %.
+#ifndef RTG_AB_NO_TIE
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+#endif
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
@@ -2224,7 +2226,14 @@ template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int
 // both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
 // the 104-register 16-wave build (dual -0.25 %, single -0.4 %, frames identical), so
 // the workgroup size is read at run time (kFill, wpb) instead of from WAVES.
-__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4) void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
+#ifdef RTG_AB_Q128
+// A/B build: the ray-queue kernel at 4 waves per SIMD (128 VGPRs, no scratch; the fifth workgroup of a CU
+// then starts only when one of the first four has finished, i.e. finds no work left)
+__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 && !QUEUE ? 5 : 4)
+#else
+__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
+#endif
+void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   const int kFill = WAVES == 4 ? static_cast<int>(blockDim.x) : WAVES * 64;  // threads of the workgroup
   const int wpb = kFill >> 6;                                                // waves of the workgroup
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

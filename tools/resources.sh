@@ -2,7 +2,7 @@
 # tools/resources.sh — per-kernel VGPR / SGPR / scratch / occupancy of rtg_kernels.hip (gfx950)
 cd "$(dirname "$0")/.."
 /opt/rocm/bin/hipcc -std=c++17 -O3 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize -Iinclude \
-  -Iraytracing-practice_amd/csrc -c raytracing-practice_amd/csrc/rtg_kernels.hip -o /tmp/rtg_res.o \
+  -Iraytracing-practice_amd/csrc ${RES_DEFS:-} -c raytracing-practice_amd/csrc/rtg_kernels.hip -o /tmp/rtg_res.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 |
   python3 -c '
 import re, sys

@@ -369,3 +369,28 @@ def test_hot_treelet_order_keeps_the_tree(lib):
     bad[5, 24] = n * 112  # a code past the array is rejected, nothing renumbered
     with pytest.raises(rtgpu.RtgError):
         lib.hot_treelet_order_host(bad, visits)
+
+
+def test_ctypes_structs_match_the_header(tmp_path):
+    """Every ctypes mirror of an include/rtgpu.h struct (python/rtgpu.py) has the C compiler's size and
+    field offsets: a field added to the header (e.g. round 4's plan words ray_queue / node_width) but
+    not to the binding would otherwise shift every later field silently."""
+    structs = sorted(n for n in dir(rtgpu) if n.startswith("rtg_") and isinstance(getattr(rtgpu, n), type)
+                     and issubclass(getattr(rtgpu, n), C.Structure))
+    assert "rtg_launch_plan" in structs and "rtg_render_desc" in structs
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "rtgpu.h"', "int main(void) {"]
+    expect = []
+    for n in structs:
+        cls = getattr(rtgpu, n)
+        lines.append(f'printf("{n} %zu\\n", sizeof({n}));')
+        expect.append(f"{n} {C.sizeof(cls)}")
+        for f in cls._fields_:
+            lines.append(f'printf("{n}.{f[0]} %zu\\n", offsetof({n}, {f[0]}));')
+            expect.append(f"{n}.{f[0]} {getattr(cls, f[0]).offset}")
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    assert [g for g in got if g] == expect

@@ -224,7 +224,8 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
 // quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
 // `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit. `brank`: the
 // closest hit's rank (-1: a sphere or none); a root equal to tmax is a miss unless this quad comes later
-// in the list than that hit (exact-t tie rule; compared on the hit path only)
+// in the list than that hit (exact-t tie rule; compared on the hit path only). brank = -2: no tie check
+// (the cache-read schedules settle ties after the call)
 __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin, float tmax, int32_t brank,
                                         int32_t& rank) {
   const float4 q0 = q[0], q4 = q[4];
@@ -249,6 +250,25 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 #endif
   return t;
 }
+
+#ifdef RTG_AB_TIE_RELOAD
+// A/B: the LDS schedule's tie check without the closest hit's rank in the traversal state: on a root
+// equal to tmax (a branch the wave skips when no lane ties) the closest hit's rank is re-read from its
+// quad record (`quads`: the LDS copy), so Trav::mat is not live across the traversal loop
+__device__ __forceinline__ float quad_t_reload(const float4* q, V3 o, V3 d, float tmin, float tmax,
+                                               const float4* quads, int32_t best) {
+  int32_t rank = -1;
+  const float t = quad_t(q, o, d, tmin, tmax, -2, rank);
+#ifndef RTG_AB_NO_TIE
+  if (t == tmax) {
+    const int32_t brank = (best >= 0 && (best & kQuadRefBit))
+                              ? ibits(quads[static_cast<int64_t>(best & ~kQuadRefBit) * 5 + 2].w) : -1;
+    if (rank <= brank) return -1.0f;
+  }
+#endif
+  return t;
+}
+#endif
 
 // Exact-t ties (rtg-f32 spec, DESIGN.md §4 "tie rule"). The reference tests the world's objects in
 // list order (hittable_list.hpp:40-64) against a shrinking interval: quad::hit accepts t ==
@@ -749,7 +769,12 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       // is a sphere or an earlier quad of the list. LDS schedule: t.mat holds the closest hit's rank and
       // quad_t rejects a losing tie on its hit path; cache-read schedules (t.mat = material): the rank
       // is re-read, only on a tie
-      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, MAT ? -2 : t.mat, qrank);
+#ifdef RTG_AB_TIE_RELOAD
+      if constexpr (!MAT)
+        th = ref == t.origin ? -1.0f : quad_t_reload(q, o, d, kTMin, t.tbest, S.quads, t.best);
+      else
+#endif
+        th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, MAT ? -2 : t.mat, qrank);
       if (MAT && th > 0.0f) m = ibits(q[1].w);
       take = th > 0.0f;
 #ifndef RTG_AB_NO_TIE

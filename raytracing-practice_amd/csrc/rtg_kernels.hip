@@ -221,6 +221,12 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   return -1.0f;
 }
 
+// A/B probe only: 1 compiles the leaf test for sphere-only scenes (no quad path); such a library renders
+// quads wrongly and is never the product build
+#ifndef RTG_SPHERES_ONLY_PROBE
+#define RTG_SPHERES_ONLY_PROBE 0
+#endif
+
 // quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
 // `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit. `brank`: the
 // closest hit's rank (-1: a sphere or none); a root equal to tmax is a miss unless this quad comes later
@@ -743,7 +749,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     t.todo = kTravDone;
     return;
   }
-  if (S.ref_mode == 1) {  // sphere-only scene, primitives stored in reference order
+  if (RTG_SPHERES_ONLY_PROBE || S.ref_mode == 1) {  // sphere-only scene, primitives stored in reference order
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;

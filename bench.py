@@ -336,6 +336,11 @@ def main():
         if args.gather_impl == "rtg":
             sys.exit("--dist-backend gloo gathers through host memory: use --gather-impl torch")
         local = local % max(1, torch.cuda.device_count())  # several ranks may share one GPU
+    elif local >= torch.cuda.device_count():
+        # one rank per GPU over RCCL: a rank without its own device cannot join (RCCL refuses two ranks
+        # on one GPU); --dist-backend gloo rehearses the flow with shared GPUs
+        sys.exit(f"[bench] rank {rank}: LOCAL_RANK {local} but {torch.cuda.device_count()} visible GPU(s); "
+                 f"--gpus {args.gpus} needs that many GPUs on the node (or --dist-backend gloo)")
     torch.cuda.set_device(local)
     if world > 1:
         if gloo:  # rehearsal of the N > 1 flow with several ranks on one GPU (tests/test_gpu.py)

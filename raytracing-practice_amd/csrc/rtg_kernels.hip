@@ -221,11 +221,10 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   return -1.0f;
 }
 
-// A/B probe only: 1 compiles the leaf test for sphere-only scenes (no quad path); such a library renders
-// quads wrongly and is never the product build
-#ifndef RTG_SPHERES_ONLY_PROBE
-#define RTG_SPHERES_ONLY_PROBE 0
-#endif
+// Primitive classes a leaf test is compiled for (leaf_step's PRIMS): any (the scene's ref_mode decides at
+// run time), spheres only, quads only. The small-scene / dual-launch LDS kernels are built once per class
+// so a sphere scene's kernel carries no quad code and the other way round (default_kernel).
+constexpr int kPrimsAny = 0, kPrimsSpheres = 1, kPrimsQuads = 2;
 
 // quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
 // `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit. `brank`: the
@@ -732,7 +731,8 @@ __device__ __forceinline__ void node_step8(Trav& t, const DevScene& S, const Stk
 
 // Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
 // LDS schedule outside the COUNT diagnostics, as for node codes).
-template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds>
+template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,
+          int PRIMS = kPrimsAny>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
   auto pop = [&]() {
@@ -749,7 +749,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     t.todo = kTravDone;
     return;
   }
-  if (RTG_SPHERES_ONLY_PROBE || S.ref_mode == 1) {  // sphere-only scene, primitives stored in reference order
+  if (PRIMS == kPrimsSpheres || (PRIMS == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
@@ -769,7 +769,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     if (COUNT) cnt.prim += 1;
     int32_t m = 0, qrank = -1;
     bool take;
-    if (ref & kQuadRefBit) {  // planar: a ray leaving a quad never hits it again
+    if (PRIMS == kPrimsQuads || (ref & kQuadRefBit)) {  // planar: a ray leaving a quad never hits it again
       const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
       // exact-t tie rule: a quad root equal to the closest hit replaces it only if that
       // is a sphere or an earlier quad of the list. LDS schedule: t.mat holds the closest hit's rank and
@@ -1409,7 +1409,7 @@ __device__ __forceinline__ void ring_batch_done(__amdgpu_buffer_rsrc_t rs, const
 // or a leaf step for the whole wave (leaf work waits until leaf_batch lanes have reached a leaf);
 // the wave switches to shading once ceil(alive * shade_batch / 64) lanes have finished their
 // closest-hit query, and lanes still traversing keep their stack and continue afterwards.
-template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM, bool RING>
+template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM, bool RING, int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
                                               const Stk& stk, WaveStats<COUNT>& w, lu32* rtab) {
   const int lane = __lane_id();
@@ -1606,7 +1606,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       if (leaf_trip && tr.todo < 0)
-        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt,
+        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM, PRIMS>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt,
                                                                            w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
@@ -2152,7 +2152,8 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 }
 
 // Schedule 3's body: the whole scene in the workgroup's LDS (render_kernel_lds with GEOM = kGeomLds).
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, bool QUEUE = false>
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, bool QUEUE = false,
+          int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCamera& C, const DevJob& J,
                                                  unsigned char* smem, int kFill, int wpb, uint64_t t0, int lane,
                                                  int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab) {
@@ -2227,15 +2228,16 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
     const int slot = blockIdx.x * wpb + wave;
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, stk, w, rtab);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, stk, w, rtab);
   } else if constexpr (QUEUE && STK16 && WIDE == 4 && !RING) {
     lu32* qb = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_queue));
     render_stream_q<LdsStack16<STACK>, COUNT, TEXF>(L, C, J, LdsStack16<STACK>{lstk16}, w, qb,
                                                     __builtin_amdgcn_readfirstlane(wave));
   } else if constexpr (STK16) {
-    render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, LdsStack16<STACK>{lstk16}, w, rtab);
+    render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack16<STACK>{lstk16}, w,
+                                                                             rtab);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
@@ -2251,7 +2253,8 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
 // persistent workgroups keep only the breadth-first top of the 4-wide tree in LDS (as many nodes as
 // fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
 // through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING, bool QUEUE = false>
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING, bool QUEUE = false,
+          int PRIMS = kPrimsAny>
 // WAVES = 4: compiled for 5 waves per SIMD (<= 96 VGPRs) and launched with 4-wave workgroups (small
 // scenes, the dual launch's second workgroup) or 16-wave ones (book-1's main launch): one binary for
 // both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
@@ -2298,7 +2301,7 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
     flush_stats<COUNT>(J, w, lane);
     trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
   } else {
-    render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, QUEUE>(S, C, J, smem, kFill, wpb, t0, lane, wave,
+    render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, QUEUE, PRIMS>(S, C, J, smem, kFill, wpb, t0, lane, wave,
                                                                           lstk, lstk16, rtab);
   }
 }
@@ -2445,15 +2448,27 @@ __global__ __launch_bounds__(256) void combine_kernel(const float* __restrict__ 
 
 constexpr int kLdsWaves = 16;  // 1024-thread persistent workgroups: 4 waves/SIMD at <= 128 VGPRs
 
-template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int WAVES = kLdsWaves>
+template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int WAVES = kLdsWaves, int PRIMS = kPrimsAny>
 KernelChoice lds_kernel(bool count, bool ring, int threads = WAVES * 64) {
   KernelChoice k;
-  k.fn = count ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM, false>)
-         : ring ? reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, true>)
-                : reinterpret_cast<const void*>(&render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, false>);
+  k.fn = count ? reinterpret_cast<const void*>(
+                     &render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM, false, false, PRIMS>)
+         : ring ? reinterpret_cast<const void*>(
+                      &render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, true, false, PRIMS>)
+                : reinterpret_cast<const void*>(
+                      &render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, false, false, PRIMS>);
   k.block = threads;
   k.dynamic_lds = true;
   return k;
+}
+
+// the 4-wave whole-scene LDS build (five 4-wave workgroups per CU, or both shapes of the dual launch) for
+// a primitive class
+template <bool TEXF>
+KernelChoice lds4_kernel(int prims, bool count, bool ring, int threads) {
+  if (prims == kPrimsSpheres) return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsSpheres>(count, ring, threads);
+  if (prims == kPrimsQuads) return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsQuads>(count, ring, threads);
+  return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsAny>(count, ring, threads);
 }
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF>
@@ -2523,12 +2538,17 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
       k.dynamic_lds = true;
       return k;
     }
-    // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds)
+    // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds),
+    // one per primitive class (kPrimsAny...: the leaf test compiled for the scene's primitives only)
+#ifndef RTG_AB_PRIMS_ANY
+    const int prims = S.ref_mode == 1 ? kPrimsSpheres : (S.ref_mode == 2 ? kPrimsQuads : kPrimsAny);
+#else
+    const int prims = kPrimsAny;  // A/B: one leaf test for every scene (round 4)
+#endif
     if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
-      return lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring, kLdsWaves * 64);
+      return lds4_kernel<false>(prims, count, ring, kLdsWaves * 64);
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU; the dual's second launch
-      return tex ? lds_kernel<kLdsStack, false, WIDE, true, kGeomLds, 4>(count, ring)
-                 : lds_kernel<kLdsStack, false, WIDE, false, kGeomLds, 4>(count, ring);
+      return tex ? lds4_kernel<true>(prims, count, ring, 4 * 64) : lds4_kernel<false>(prims, count, ring, 4 * 64);
     return tex ? lds_kernel<kLdsStack, false, WIDE, true>(count, ring) : lds_kernel<kLdsStack, false, WIDE, false>(count, ring);
   }
   if (stack > 32 || J.lds_stack > stack) return {};

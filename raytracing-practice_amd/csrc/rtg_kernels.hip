@@ -2294,9 +2294,10 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
       int32_t* tstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * J.lds_stack * 64 + lane;
       const SpillStack<STACK> stk{tstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                   J.lds_stack, J.lds_stack + J.spill_depth};
-      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, stk, w, rtab);
+      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, stk, w, rtab);
     } else {
-      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
+      render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w,
+                                                                                rtab);
     }
     flush_stats<COUNT>(J, w, lane);
     trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
@@ -2505,11 +2506,19 @@ KernelChoice treelet_kernel(const DevScene& S, const DevJob& J, bool count) {
                  : lds_kernel<kLdsStack, false, 8, false, kGeomTreelet>(count, ring);
   }
   if (S.node_width != 4) return {};
+  // sphere-only scenes (the 1M field) get a build without the quad test (kPrimsSpheres, as default_kernel)
+#ifndef RTG_AB_PRIMS_ANY
+  const bool spheres = S.ref_mode == 1 && !tex;
+#else
+  const bool spheres = false;
+#endif
   if (spill)
     return tex ? lds_kernel<kLdsStack, true, 4, true, kGeomTreelet>(count, ring)
-               : lds_kernel<kLdsStack, true, 4, false, kGeomTreelet>(count, ring);
+               : spheres ? lds_kernel<kLdsStack, true, 4, false, kGeomTreelet, kLdsWaves, kPrimsSpheres>(count, ring)
+                         : lds_kernel<kLdsStack, true, 4, false, kGeomTreelet>(count, ring);
   return tex ? lds_kernel<kLdsStack, false, 4, true, kGeomTreelet>(count, ring)
-             : lds_kernel<kLdsStack, false, 4, false, kGeomTreelet>(count, ring);
+             : spheres ? lds_kernel<kLdsStack, false, 4, false, kGeomTreelet, kLdsWaves, kPrimsSpheres>(count, ring)
+                       : lds_kernel<kLdsStack, false, 4, false, kGeomTreelet>(count, ring);
 }
 
 // The default schedules: persistent LDS kernel (16 LDS stack entries) or the plain grid (16, or 32

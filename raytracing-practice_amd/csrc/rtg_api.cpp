@@ -1051,6 +1051,10 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.tex_full = 0;
   for (int32_t t = 0; t < desc->num_textures; ++t)
     if (desc->textures[t].type == RTG_TEX_IMAGE || desc->textures[t].type == RTG_TEX_NOISE) s->dev.tex_full = 1;
+  s->dev.diffuse_only = 1;
+  for (int32_t m = 0; m < desc->num_materials; ++m)
+    if (desc->materials[m].type == RTG_MAT_METAL || desc->materials[m].type == RTG_MAT_DIELECTRIC)
+      s->dev.diffuse_only = 0;
   s->dev.num_perlins = static_cast<int32_t>(hs.perlin_perm.size() / 768);
   s->num_cus = prop.multiProcessorCount;
   // trees too large for any LDS schedule render on the treelet schedule: keep their node array on the

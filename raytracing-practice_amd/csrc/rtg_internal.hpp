@@ -165,6 +165,7 @@ struct DevScene {
   // (single-kind scenes store primitives in reference order, so the indirection is the identity)
   int32_t ref_mode;
   int32_t tex_full;  // 1 when some texture is an image or noise texture (kernel variant selector)
+  int32_t diffuse_only;  // 1 when no material is metal or dielectric (kernel variant selector)
   int32_t num_perlins;  // perlin tables (256 gradients + 3 x 256 permutations each)
   // 4-wide trees: inner-node codes are byte offsets from `nodes`, the root's is root_code (0 in
   // HBM; the persistent kernel rebases its LDS copy so codes are absolute LDS addresses) and every

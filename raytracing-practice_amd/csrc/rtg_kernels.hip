@@ -221,10 +221,11 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   return -1.0f;
 }
 
-// Primitive classes a leaf test is compiled for (leaf_step's PRIMS): any (the scene's ref_mode decides at
-// run time), spheres only, quads only. The small-scene / dual-launch LDS kernels are built once per class
-// so a sphere scene's kernel carries no quad code and the other way round (default_kernel).
-constexpr int kPrimsAny = 0, kPrimsSpheres = 1, kPrimsQuads = 2;
+// Scene classes a kernel is compiled for (PRIMS): bits 0-1 the primitives its leaf test and shading
+// handle — any (the scene's ref_mode decides at run time), spheres only, quads only — and bit 2 set when
+// no material is metal or dielectric. The small-scene / dual-launch LDS kernels are built per class so
+// a scene's kernel carries no code for what the scene lacks (default_kernel).
+constexpr int kPrimsAny = 0, kPrimsSpheres = 1, kPrimsQuads = 2, kPrimsKind = 3, kPrimsDiffuse = 4;
 
 // quad::hit (quad.hpp:44-114); plane distance D - n.O formed in f64.
 // `rank`: the quad's list index (its record's v.w, DESIGN.md §4 "tie rule"), set with a hit. `brank`: the
@@ -749,7 +750,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     t.todo = kTravDone;
     return;
   }
-  if (PRIMS == kPrimsSpheres || (PRIMS == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
+  if ((PRIMS & kPrimsKind) == kPrimsSpheres || ((PRIMS & kPrimsKind) == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
@@ -769,7 +770,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     if (COUNT) cnt.prim += 1;
     int32_t m = 0, qrank = -1;
     bool take;
-    if (PRIMS == kPrimsQuads || (ref & kQuadRefBit)) {  // planar: a ray leaving a quad never hits it again
+    if ((PRIMS & kPrimsKind) == kPrimsQuads || (ref & kQuadRefBit)) {  // planar: a ray leaving a quad never hits it again
       const float4* q = S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
       // exact-t tie rule: a quad root equal to the closest hit replaces it only if that
       // is a sphere or an earlier quad of the list. LDS schedule: t.mat holds the closest hit's rank and
@@ -1074,12 +1075,15 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
 // (ray_color's emission-only return, camera.hpp:213-216, or a miss handled by the caller).
 // MAT: `mat` is the hit's material (Trav::mat), so its record is fetched beside the primitive's
 // (the cache-read schedules: two independent loads instead of a dependent pair)
-template <bool FULL, bool MAT = false>
+// PRIMS: the scene class (kPrimsAny ...): sphere-only kernels shade spheres only, quad-only ones quads
+// only (chosen only without a sphere occluder), diffuse-only ones have no metal / dielectric code
+template <bool FULL, bool MAT = false, int PRIMS = kPrimsAny>
 __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, int32_t mat_hit = 0) {
   V3 p, outward;
   float u = 0.0f, v = 0.0f;
   int mat;
-  bool sphere = !(ref & kQuadRefBit);
+  const bool sphere = (PRIMS & kPrimsKind) == kPrimsSpheres ||
+                      ((PRIMS & kPrimsKind) == kPrimsAny && !(ref & kQuadRefBit));
   if (sphere) {
     const float4* s = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
     const float4 s0 = s[0], s1 = s[1];
@@ -1121,10 +1125,11 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
     return false;
   }
   V3 dir, att;
-  if (type == RTG_MAT_LAMBERTIAN || type == RTG_MAT_METAL) {
+  constexpr bool kDiffuse = (PRIMS & kPrimsDiffuse) != 0;
+  if (type == RTG_MAT_LAMBERTIAN || (!kDiffuse && type == RTG_MAT_METAL)) {
     // both scatter around a random unit vector: one sampling code path for the lanes of either
     const V3 r = random_unit_vector(ps.rng);
-    if (type == RTG_MAT_LAMBERTIAN) {
+    if (kDiffuse || type == RTG_MAT_LAMBERTIAN) {
       dir = add(n, r);
       // near_zero with the reference's fabs(e[1] < s) quirk (vec3.hpp:70-77, H5)
       const float s = 1e-8f;
@@ -1138,7 +1143,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
       att = xyz(m1);
       if (!(dot(dir, n) > 0.0f)) return false;  // absorbed: color_from_emission == 0
     }
-  } else if (type == RTG_MAT_DIELECTRIC) {
+  } else if (!kDiffuse && type == RTG_MAT_DIELECTRIC) {
     att = v3(1.0f, 1.0f, 1.0f);
     const float eta = m0.w;
     const float ri = front ? div_rn(1.0f, eta) : eta;
@@ -1652,7 +1657,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         alive_path = false;
       } else {
         if (COUNT) ++w.hits;
-        alive_path = shade<TEXF, GEOM != kGeomLds>(S, ps, tr.best, tr.tbest, tr.mat);
+        alive_path = shade<TEXF, GEOM != kGeomLds, PRIMS>(S, ps, tr.best, tr.tbest, tr.mat);
         if (alive_path && --ps.depth <= 0) alive_path = false;
       }
       uint64_t t_end = 0;
@@ -2467,9 +2472,17 @@ KernelChoice lds_kernel(bool count, bool ring, int threads = WAVES * 64) {
 // a primitive class
 template <bool TEXF>
 KernelChoice lds4_kernel(int prims, bool count, bool ring, int threads) {
-  if (prims == kPrimsSpheres) return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsSpheres>(count, ring, threads);
-  if (prims == kPrimsQuads) return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsQuads>(count, ring, threads);
-  return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsAny>(count, ring, threads);
+  switch (prims) {
+    case kPrimsSpheres: return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsSpheres>(count, ring, threads);
+    case kPrimsQuads: return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsQuads>(count, ring, threads);
+    case kPrimsAny | kPrimsDiffuse:
+      return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsAny | kPrimsDiffuse>(count, ring, threads);
+    case kPrimsSpheres | kPrimsDiffuse:
+      return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsSpheres | kPrimsDiffuse>(count, ring, threads);
+    case kPrimsQuads | kPrimsDiffuse:
+      return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsQuads | kPrimsDiffuse>(count, ring, threads);
+    default: return lds_kernel<kLdsStack, false, 4, TEXF, kGeomLds, 4, kPrimsAny>(count, ring, threads);
+  }
 }
 
 template <int STACK, bool SPILL, int WIDE, bool TEXF>
@@ -2550,7 +2563,13 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
     // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds),
     // one per primitive class (kPrimsAny...: the leaf test compiled for the scene's primitives only)
 #ifndef RTG_AB_PRIMS_ANY
-    const int prims = S.ref_mode == 1 ? kPrimsSpheres : (S.ref_mode == 2 ? kPrimsQuads : kPrimsAny);
+    // (a quad-only tree with a sphere occluder beside it shades spheres too: kPrimsAny)
+    const int kind = S.ref_mode == 1 ? kPrimsSpheres : (S.ref_mode == 2 && S.occluder < 0 ? kPrimsQuads : kPrimsAny);
+#ifndef RTG_AB_NO_DIFFUSE_CLASS
+    const int prims = kind | (S.diffuse_only ? kPrimsDiffuse : 0);
+#else
+    const int prims = kind;
+#endif
 #else
     const int prims = kPrimsAny;  // A/B: one leaf test for every scene (round 4)
 #endif

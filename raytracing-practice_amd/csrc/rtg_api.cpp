@@ -51,7 +51,7 @@ constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
 constexpr int64_t kRingAutoBytes = int64_t(4) << 30;  // full-frame partials above this: the tile ring
-constexpr int kNumCounters = 28;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring, [26] ray queues)
+constexpr int kNumCounters = 28;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring)
 // gfx950 allocates a workgroup's LDS in 1280-byte granules (160 KB = 128 of them): measured with the
 // dual launch, whose two workgroups stop sharing a CU exactly when the rounded sizes pass 160 KB
 constexpr int kLdsGranule = 1280;
@@ -235,9 +235,6 @@ Knobs read_knobs() {
   if (num("RTG_TILE_SLOTS", 0, 65536, &ts) && (ts & (ts - 1)) == 0) k.tile_slots = ts;
   num("RTG_TREELET_STACK", 4, 16, &k.treelet_stack);
   num("RTG_TREELET_HOT", 0, 1, &k.treelet_hot);
-  num("RTG_RAY_QUEUE", 0, 1, &k.ray_queue);
-  num("RTG_Q_DEPOSIT", 1, 64, &k.q_deposit);
-  num("RTG_Q_SHADERS", 1, 8, &k.q_shaders);
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -1131,14 +1128,6 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   if (c[5] != 0) return fail(RTG_E_INVALID, "corrupt BVH child code met during traversal");
   if (c[24] != 0)
     return fail(RTG_E_HIP, "tile-ring slot waits timed out (frame incomplete) in " + std::to_string(c[24]) + " waves");
-  if (c[26] != 0) {
-    const unsigned long long r = c[27];
-    char buf[200];
-    std::snprintf(buf, sizeof buf, " (first: kind %llu, shade queue %llu, trace queue %llu, units %llu, reports %llu, "
-                  "own rays %llu)", r & 15ull, (r >> 4) & 1023ull, (r >> 14) & 1023ull, (r >> 24) & 0xffffull,
-                  (r >> 40) & 15ull, (r >> 44) & 127ull);
-    return fail(RTG_E_HIP, "ray-queue waits timed out (frame incomplete) in " + std::to_string(c[26]) + " waves" + buf);
-  }
   if (c[7] != 0)
     return fail(RTG_E_UNSUPPORTED, "the 16-bit LDS stack layout cannot hold this tree's codes in " +
                                        std::to_string(c[7]) + " workgroups (nothing rendered)");
@@ -1215,7 +1204,6 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
 
   DevJob& dj = P->dj;
   dj = DevJob{};
-  dj.lds_queue = -1;
   dj.seed_mix = mix64(job->seed);
   dj.row_begin = job->row_begin;
   dj.row_stride = job->row_stride;
@@ -1415,34 +1403,6 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     j4.lds_ring = l4[9];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
-  // ray queues (RTG_RAY_QUEUE prototype) on the LDS schedule with 16-bit stacks, no image /
-  // noise textures, one-shot frames without the tile ring: the small-scene shape (five 4-wave workgroups
-  // per CU: three tracing waves + one shading wave each), or one 16-wave workgroup per CU whose queues
-  // take the LDS of the dual launch's second workgroup (book-1: 16 - RTG_Q_SHADERS tracing waves). The
-  // queues go after the scene copy, as large as the shape still allows.
-  if (K.ray_queue && variant == 3 && dj.stack_esz == 2 && !dscene.tex_full && dj.ring_log2 < 0 && !P->skip_kernel) {
-    const int qoff = (lds_bytes + 15) & ~15;
-    const bool small = dj.lds_waves == 4 && lds_wgs == kSmallSceneWgs && lds4 < 0;
-    const bool big = dj.lds_waves == kLdsWaves && lds_wgs == 1;
-    const int tracers = small ? kQTracerWaves : kLdsWaves - K.q_shaders;
-    for (const int T : {512, 256, 128, 64, 32}) {
-      if (!small && !big) break;
-      const int Sq = small ? std::min(64, T) : 128;  // queue capacities: powers of two
-      const int qbytes = (kQCtl + kQEntryDw * (Sq + T)) * 4;
-      const bool fits = small ? lds_alloc(qoff + qbytes) * kSmallSceneWgs <= kLdsPerCu
-                              : lds_alloc(qoff + qbytes) <= kLdsPerCu;
-      if (!fits || (small && T > 128)) continue;
-      dj.lds_queue = qoff;
-      dj.q_shade = Sq;
-      dj.q_trace = T;
-      dj.q_tracers = tracers;
-      dj.q_rmax = tracers * 64 + Sq + T;  // no queue deadlock below this (rtg_kernels.hip)
-      dj.q_deposit = K.q_deposit;
-      lds_bytes = qoff + qbytes;
-      lds4 = -1;  // the queues replace the dual launch's second workgroup
-      break;
-    }
-  }
   P->j4 = j4;
   P->variant = variant;
   P->lds_bytes = lds_bytes;
@@ -1612,7 +1572,7 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
                                                      : static_cast<int64_t>(P.out_bytes) * P.dj.chunks;
   out->tile_slots = P.ring_slots;
   out->num_cus = s->num_cus;
-  out->ray_queue = P.dj.lds_queue >= 0 ? P.dj.q_shade : 0;
+  out->ray_queue = 0;  // retired in round 5 (tools/experiments/ray_queue.patch)
   out->node_width = P.dscene.node_width;
   if (P.variant == 5) {
     out->treelet_hot = s->treelet_key == treelet_key(cam, job) ? 1 : 0;

@@ -211,13 +211,6 @@ hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int3
 
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
 
-// Ray queues of the small-scene schedule (RTG_RAY_QUEUE prototype, rtg_kernels.hip render_stream_q):
-// control words (16 B aligned: the entries follow them), dwords per queue entry (path state + unit +
-// hit), the tracing waves of a 4-wave workgroup (the fourth shades)
-constexpr int kQCtl = 16;
-constexpr int kQEntryDw = 28;  // 112 B per queue entry (seven 16-B rows; the trace queue leaves row 6 unused)
-constexpr int kQTracerWaves = 3;  // of a 4-wave workgroup (small scenes); 16-wave ones: 16 - RTG_Q_SHADERS
-
 // Interleaved row shards of the multi-GPU frame (rtg_shard_layout, rtg_render_frame, rtg_gather_rows):
 // rank r of N renders image rows r, r+N, ...; every shard is padded to P = ceil(H/N) rows.
 struct ShardLayout {
@@ -250,10 +243,6 @@ struct Knobs {
   int tile_slots = -1;          // RTG_TILE_SLOTS 0 (full-frame partials) | 1..65536 (-1: by chunks)
   int treelet_stack = 16;       // RTG_TREELET_STACK 4..16: LDS stack entries of the treelet schedule
                                 // (fewer: more treelet nodes, more spill traffic; spilling trees only)
-  int ray_queue = 0;            // RTG_RAY_QUEUE 0 | 1: cross-wave ray queues in the small-scene schedule
-                                // (prototype, DESIGN.md §6 "rays between waves")
-  int q_deposit = 16;           // RTG_Q_DEPOSIT 1..64: finished lanes that end a tracer wave's trips
-  int q_shaders = 4;            // RTG_Q_SHADERS 1..8: shading waves of a 16-wave ray-queue workgroup
   int treelet_hot = 1;          // RTG_TREELET_HOT 0 | 1: treelet of the most-visited nodes for the
                                 // camera (a probe render counts node visits), 0: breadth-first top
   std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
@@ -271,8 +260,7 @@ struct DevJob {
   // [6] persistent kernels' tile counter, [7] workgroups that could not run the 16-bit LDS stack
   // layout (codes past 16 bits: RTG_E_UNSUPPORTED, nothing rendered), [8..23] schedule diagnostics,
   // [24] tile-ring waits that timed out (RTG_E_INTERNAL: frame incomplete), [25] batches that found
-  // their ring slot still owned by an earlier tile (waits; diagnostic), [26] ray-queue waits that timed
-  // out (RTG_RAY_QUEUE: RTG_E_HIP, frame incomplete)
+  // their ring slot still owned by an earlier tile (waits; diagnostic)
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 64-pixel tiles per shard row of tiles
@@ -305,14 +293,6 @@ struct DevJob {
   int32_t stack_esz;                         // persistent kernels: bytes per LDS stack entry (2 or 4)
   int32_t lds_stacks;                        // persistent kernels: byte offset of the traversal stacks in LDS
   int32_t lds_ring;                          // RING kernels: byte offset of the per-wave batch tables (64 B each)
-  // ray queues (RTG_RAY_QUEUE, small-scene schedule): byte offset of the workgroup's queue area in LDS
-  // (-1: off), capacities (powers of two) of the shade queue (rays that finished traversal) and of the
-  // trace queue (shaded rays waiting for a tracer lane), the most unit contexts a workgroup keeps in
-  // flight, and the finished tracer lanes that end a tracer wave's trips
-  int32_t lds_queue;
-  int32_t q_shade, q_trace, q_rmax, q_deposit;
-  int32_t q_tracers;  // waves 0 .. q_tracers - 1 trace, the others shade
-
 };
 
 }  // namespace rtg

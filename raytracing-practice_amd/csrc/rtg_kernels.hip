@@ -1709,429 +1709,6 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   if (ring && (exhausted_by_timeout || e_used != 0) && lane == 0) atomicAdd(&J.counters[24], 1ull);
 }
 
-// ---- Rays between waves (RTG_RAY_QUEUE; VERDICT r03 item 4, a prototype on the small-scene schedule) ----
-// In render_stream a wave owns its 64 rays: a lane whose traversal has finished waits, idle, until the
-// wave's shading batch, and a shading batch runs with the still-traversing lanes idle (lane utilisation
-// 0.45-0.49 on every config). Here the rays move between the waves of a workgroup through
-// two LDS queues: waves 0..2 only trace; when a few of a tracer wave's lanes have finished their
-// closest-hit query, those lanes deposit their ray (path state + hit + its unit: pixel, sample range,
-// chunk sum) in the SHADE queue and take a shaded ray from the TRACE queue (or, when that is empty, a
-// fresh unit), so tracer lanes do not wait for shading; wave 3 only shades: it takes up to 64 rays from
-// the shade queue, shades them with full waves, finishes paths and units exactly as render_stream does
-// (a unit's samples stay in order in one context, so every chunk sum is bit-identical), and puts the
-// continuing rays in the trace queue. Queues: 112-B entries (seven 16-B rows, conflict-free for
-// consecutive slots), ring indices under a workgroup lock. A workgroup keeps at most q_rmax unit contexts in flight
-// (192 tracer lanes + both queue capacities): with that many, a tracer lane can always deposit or the
-// shader can always hand rays back, so the queues never deadlock. Every wait is bounded (counters[26]).
-// control words (kQCtl): [0] lock, [1] shade head, [2] shade count, [3] trace head, [4] trace count,
-// [5] unit contexts in flight, [6] tracer waves that handed out their last unit
-
-struct RayQueues {
-  lu32* ctl;
-  lu32* sq;  // S entries of kQEntryDw dwords
-  lu32* tq;  // T entries
-  int S, T;
-};
-
-__device__ __forceinline__ uint32_t q_ld(lu32* a) {
-  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void q_st(lu32* a, uint32_t v) {
-  __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// A queue wait that timed out: counted in counters[26]; the first one also leaves its kind and the
-// workgroup's queue state in counters[27] (kind | shade count << 4 | trace count << 14 | units in flight
-// << 24 | tracer reports << 40 | the wave's own rays << 44), which the host reports in the error
-__device__ __forceinline__ void q_timeout(const DevJob& J, lu32* ctl, uint32_t kind, uint32_t own) {
-  atomicAdd(&J.counters[26], 1ull);
-  const unsigned long long rec =
-      static_cast<unsigned long long>(kind) | (static_cast<unsigned long long>(q_ld(ctl + 2) & 1023u) << 4) |
-      (static_cast<unsigned long long>(q_ld(ctl + 4) & 1023u) << 14) |
-      (static_cast<unsigned long long>(q_ld(ctl + 5) & 0xffffu) << 24) |
-      (static_cast<unsigned long long>(q_ld(ctl + 6) & 15u) << 40) | (static_cast<unsigned long long>(own & 127u) << 44);
-  atomicCAS(&J.counters[27], 0ull, rec);
-}
-
-// Workgroup lock (ctl[0]) for one wave; false when it could not be taken (bounded: counters[26]).
-__device__ __forceinline__ bool q_lock(const DevJob& J, lu32* ctl) {
-  uint32_t ok = 1;
-  if (__lane_id() == 0) {
-    uint32_t spins = 0;
-    for (;;) {
-      uint32_t expect = 0;
-      if (__hip_atomic_compare_exchange_strong(ctl, &expect, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP))
-        break;
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 22)) {
-        ok = 0;
-        q_timeout(J, ctl, 1u, 0u);
-        break;
-      }
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  return __builtin_amdgcn_readfirstlane(ok) != 0;
-}
-__device__ __forceinline__ void q_unlock(lu32* ctl) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (__lane_id() == 0) __hip_atomic_store(ctl, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// A unit context (its current path and the unit's own state) in slot i of a queue: seven 16-B rows per
-// entry (112 B, an odd number of 16-B bank slots, so the ds_write_b128 / ds_read_b128 of consecutive
-// slots spread over every bank; 7 LDS operations per copy instead of 26)
-//   row 0: o.xyz d.x | 1: d.yz time T.x | 2: T.yz L.xy | 3: L.z depth origin rng.lo
-//   row 4: rng.hi acc.xyz | 5: px (sample | s_end << 16) chunk tbest | 6: best (shade queue only)
-struct UnitCtx {
-  PathState ps;
-  V3 acc;
-  uint32_t px;
-  int sample, s_end, chunk;
-};
-typedef unsigned int qu4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void q_row_st(lu32* q, int i, int r, qu4 v) {
-  *reinterpret_cast<__attribute__((address_space(3))) qu4*>(q + (i * kQEntryDw + 4 * r)) = v;
-}
-__device__ __forceinline__ qu4 q_row_ld(lu32* q, int i, int r) {
-  return *reinterpret_cast<__attribute__((address_space(3))) const qu4*>(q + (i * kQEntryDw + 4 * r));
-}
-__device__ __forceinline__ void q_put(lu32* q, int i, const UnitCtx& u, bool hit, float t, int32_t best) {
-  auto f = [](float x) { return __float_as_uint(x); };
-  q_row_st(q, i, 0, qu4{f(u.ps.o.x), f(u.ps.o.y), f(u.ps.o.z), f(u.ps.d.x)});
-  q_row_st(q, i, 1, qu4{f(u.ps.d.y), f(u.ps.d.z), f(u.ps.time), f(u.ps.T.x)});
-  q_row_st(q, i, 2, qu4{f(u.ps.T.y), f(u.ps.T.z), f(u.ps.L.x), f(u.ps.L.y)});
-  q_row_st(q, i, 3, qu4{f(u.ps.L.z), static_cast<uint32_t>(u.ps.depth), static_cast<uint32_t>(u.ps.origin),
-                        static_cast<uint32_t>(u.ps.rng)});
-  q_row_st(q, i, 4, qu4{static_cast<uint32_t>(u.ps.rng >> 32), f(u.acc.x), f(u.acc.y), f(u.acc.z)});
-  q_row_st(q, i, 5, qu4{u.px, static_cast<uint32_t>(u.sample) | (static_cast<uint32_t>(u.s_end) << 16),
-                        static_cast<uint32_t>(u.chunk), f(t)});
-  if (hit) q_row_st(q, i, 6, qu4{static_cast<uint32_t>(best), 0u, 0u, 0u});
-}
-__device__ __forceinline__ void q_get(lu32* q, int i, UnitCtx& u, bool hit, float& t, int32_t& best) {
-  auto f = [](uint32_t x) { return __uint_as_float(x); };
-  const qu4 r0 = q_row_ld(q, i, 0), r1 = q_row_ld(q, i, 1), r2 = q_row_ld(q, i, 2), r3 = q_row_ld(q, i, 3);
-  const qu4 r4 = q_row_ld(q, i, 4), r5 = q_row_ld(q, i, 5);
-  u.ps.o = v3(f(r0.x), f(r0.y), f(r0.z));
-  u.ps.d = v3(f(r0.w), f(r1.x), f(r1.y));
-  u.ps.time = f(r1.z);
-  u.ps.T = v3(f(r1.w), f(r2.x), f(r2.y));
-  u.ps.L = v3(f(r2.z), f(r2.w), f(r3.x));
-  u.ps.depth = static_cast<int>(r3.y);
-  u.ps.origin = static_cast<int32_t>(r3.z);
-  u.ps.rng = static_cast<uint64_t>(r3.w) | (static_cast<uint64_t>(r4.x) << 32);
-  u.acc = v3(f(r4.y), f(r4.z), f(r4.w));
-  u.px = r5.x;
-  u.sample = static_cast<int>(r5.y & 0xffffu);
-  u.s_end = static_cast<int>(r5.y >> 16);
-  u.chunk = static_cast<int>(r5.z);
-  if (hit) {
-    t = f(r5.w);
-    best = static_cast<int32_t>(q_row_ld(q, i, 6).x);
-  }
-}
-
-// A unit's result: its chunk partial sum (or the pixel mean when the pixel has one chunk).
-__device__ __forceinline__ void store_unit(const DevCamera& C, const DevJob& J, const UnitCtx& u) {
-  const int64_t pix = static_cast<int64_t>(px_lr(u.px)) * C.width + px_i(u.px);
-  if (J.partial == nullptr) {
-    float* o = J.out + pix * 3;
-    o[0] = C.scale * u.acc.x;
-    o[1] = C.scale * u.acc.y;
-    o[2] = C.scale * u.acc.z;
-  } else {
-    float* o = J.partial + (static_cast<int64_t>(u.chunk) * J.row_count * C.width + pix) * 3;
-    o[0] = u.acc.x;
-    o[1] = u.acc.y;
-    o[2] = u.acc.z;
-  }
-}
-
-// The shading wave: batches of up to 64 rays from the shade queue, shaded with full lanes.
-template <bool COUNT, bool TEXF>
-__device__ __forceinline__ void q_shader(const DevScene& S, const DevCamera& C, const DevJob& J, const RayQueues& Q,
-                                         WaveStats<COUNT>& w) {
-  const int lane = __lane_id();
-  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
-  uint32_t idle = 0;
-  for (;;) {
-    // peek without the lock: an idle wave that took the lock on every poll kept it busy enough that
-    // a working wave could not get it (round-4 GPU tests: lock waits timed out in small-scene
-    // workgroups, where two of the three tracers and the shader idle most of the frame)
-    if (q_ld(Q.ctl + 2) == 0u) {
-      const uint32_t reports = __hip_atomic_load(Q.ctl + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (reports >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
-      __builtin_amdgcn_s_sleep(4);
-      if (++idle > (1u << 24)) {
-        if (lane == 0) q_timeout(J, Q.ctl, 2u, 0u);
-        return;
-      }
-      continue;
-    }
-    if (!q_lock(J, Q.ctl)) return;
-    const uint32_t head = q_ld(Q.ctl + 1), cnt = q_ld(Q.ctl + 2), tcnt = q_ld(Q.ctl + 4);
-    // a full batch, or what there is when no shaded ray waits for the tracers (they may be starving)
-    const uint32_t full = min(64u, static_cast<uint32_t>(Q.S));
-    const uint32_t take = cnt >= full ? full : (tcnt == 0u ? cnt : 0u);
-    UnitCtx u;
-    float t = 0.0f;
-    int32_t best = -1;
-    const bool mine = static_cast<uint32_t>(lane) < take;
-    if (mine) q_get(Q.sq, static_cast<int>((head + lane) & (Q.S - 1)), u, true, t, best);
-    if (take != 0u) {
-      if (lane == 0) {
-        q_st(Q.ctl + 1, (head + take) & (Q.S - 1));
-        q_st(Q.ctl + 2, cnt - take);
-      }
-    }
-    q_unlock(Q.ctl);
-    if (take == 0u) {
-      // done once every tracer wave has handed out its last unit and no unit is in flight. The report
-      // count is loaded with acquire (the tracers add to it with release, after adding their units to
-      // ctl[5]), so seeing every report means seeing every unit: loaded in the other order (relaxed
-      // loads may be reordered) a shading wave could read ctl[5] before a tracer's last units and the
-      // report after them, and leave those units unshaded (round-4 GPU tests: ray-queue waits timed out)
-      const uint32_t reports = __hip_atomic_load(Q.ctl + 6, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (reports >= static_cast<uint32_t>(J.q_tracers) && q_ld(Q.ctl + 5) == 0u) return;
-      __builtin_amdgcn_s_sleep(2);
-      if (++idle > (1u << 24)) {
-        if (lane == 0) q_timeout(J, Q.ctl, 2u, 0u);
-        return;
-      }
-      continue;
-    }
-    idle = 0;
-    bool cont = false, unit_done = false;
-    if (mine) {
-      ++w.segs;
-      bool alive_path;
-      if (best < 0) {
-        u.ps.L = vfma(u.ps.T, bg, u.ps.L);
-        alive_path = false;
-      } else {
-        if (COUNT) ++w.hits;
-        alive_path = shade<TEXF>(S, u.ps, best, t);
-        if (alive_path && --u.ps.depth <= 0) alive_path = false;
-      }
-      cont = alive_path;
-      if (!alive_path) {
-        u.acc = add(u.acc, u.ps.L);
-        ++u.sample;
-        if (u.sample < u.s_end) {
-          start_pixel_sample(u.ps, C, J, u.px, static_cast<uint32_t>(u.sample));
-          cont = true;
-        } else {
-          store_unit(C, J, u);
-          unit_done = true;
-          ++w.pixels;
-        }
-      }
-    }
-    const uint32_t ndone = static_cast<uint32_t>(__popcll(ballot(unit_done)));
-    // the continuing rays into the trace queue, as many as it has room for each time (a trace queue
-    // smaller than a batch, as small scenes' LDS allows, takes a batch in parts); the workgroup's q_rmax
-    // guarantees room eventually, the wait is bounded
-    uint32_t spins = 0;
-    for (;;) {
-      const uint64_t pm = ballot(cont);
-      const uint32_t npush = static_cast<uint32_t>(__popcll(pm));
-      if (npush == 0u) break;
-      if (!q_lock(J, Q.ctl)) return;
-      const uint32_t th = q_ld(Q.ctl + 3), tc = q_ld(Q.ctl + 4);
-      const uint32_t put = min(npush, static_cast<uint32_t>(Q.T) - tc);
-      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(pm >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(pm), 0u)));
-      if (cont && static_cast<uint32_t>(rank) < put) {
-        q_put(Q.tq, static_cast<int>((th + tc + rank) & (Q.T - 1)), u, false, 0.0f, 0);
-        cont = false;
-      }
-      if (lane == 0 && put != 0u) q_st(Q.ctl + 4, tc + put);
-      q_unlock(Q.ctl);
-      if (put == npush) break;
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 22)) {
-        if (lane == 0) q_timeout(J, Q.ctl, 3u, npush);
-        return;
-      }
-    }
-    if (ndone != 0u && lane == 0)
-      __hip_atomic_fetch_sub(Q.ctl + 5, ndone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-
-// A tracing wave: render_stream's hand-out and trip loop, with finished lanes depositing their ray in
-// the shade queue and refilling from the trace queue (then from fresh units) instead of shading.
-template <class Stk, bool COUNT, bool TEXF>
-__device__ __forceinline__ void q_tracer(const DevScene& S, const DevCamera& C, const DevJob& J, const Stk& stk,
-                                         const RayQueues& Q, WaveStats<COUNT>& w) {
-  const int lane = __lane_id();
-  const int num_batches = J.num_tiles * J.chunks;
-  UnitCtx u;
-  u.acc = v3(0.0f, 0.0f, 0.0f);
-  u.px = 0;
-  u.sample = 0, u.s_end = 0, u.chunk = 0;
-  u.ps = {};
-  auto has = [&]() { return u.s_end != 0; };
-  bool fresh = false, arrived = false;
-  int bx = 0, by = 0, bc = 0, k_next = 64;
-  bool exhausted = false, reported = false;
-  Trav tr = {};
-  tr.todo = kTravDone;
-  uint32_t idle = 0;
-  int backlog = 0;  // finished lanes the shade queue had no room for at the last deposit
-  for (;;) {
-    // 1. deposit finished rays, refill empty lanes from the trace queue (one lock)
-    const bool fin = has() && !trav_active(tr);
-    const uint64_t fm = ballot(fin);
-    bool tq_empty = true;
-    backlog = 0;
-    // the lock only when this wave has rays to deposit or empty lanes and shaded rays wait (peeked
-    // without the lock): idle waves polling under the lock starved the working ones
-    const bool refill = ballot(!has()) != 0 && q_ld(Q.ctl + 4) != 0u;
-    if (fm != 0 || refill) {
-      if (!q_lock(J, Q.ctl)) return;
-      const uint32_t sh = q_ld(Q.ctl + 1), sc = q_ld(Q.ctl + 2);
-      const uint32_t take = min(static_cast<uint32_t>(__popcll(fm)), static_cast<uint32_t>(Q.S) - sc);
-      const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(fm >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(fm), 0u)));
-      if (fin && static_cast<uint32_t>(rank) < take) {
-        q_put(Q.sq, static_cast<int>((sh + sc + rank) & (Q.S - 1)), u, true, tr.tbest, tr.best);
-        u.s_end = 0;  // the lane is empty now
-      }
-      const uint64_t em = ballot(!has());
-      const uint32_t th = q_ld(Q.ctl + 3), tc = q_ld(Q.ctl + 4);
-      const uint32_t take2 = min(static_cast<uint32_t>(__popcll(em)), tc);
-      const int rank2 = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(em >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(em), 0u)));
-      if (!has() && static_cast<uint32_t>(rank2) < take2) {
-        float t_unused;
-        int32_t b_unused;
-        q_get(Q.tq, static_cast<int>((th + rank2) & (Q.T - 1)), u, false, t_unused, b_unused);
-        arrived = true;
-      }
-      if (lane == 0) {
-        q_st(Q.ctl + 2, sc + take);
-        q_st(Q.ctl + 3, (th + take2) & (Q.T - 1));
-        q_st(Q.ctl + 4, tc - take2);
-      }
-      tq_empty = tc == take2;
-      backlog = __popcll(fm) - static_cast<int>(take);
-      q_unlock(Q.ctl);
-    }
-    // 2. fresh units for lanes still empty, while the trace queue is empty and the workgroup's budget of
-    // units in flight allows (render_stream's batch hand-out)
-    uint64_t want = ballot(!has());
-    if (want != 0 && tq_empty && !(exhausted && k_next >= 64)) {
-      const uint32_t rays = q_ld(Q.ctl + 5);
-      int budget = rays < static_cast<uint32_t>(J.q_rmax) ? J.q_rmax - static_cast<int>(rays) : 0;
-      int started = 0;
-      while (want != 0 && budget > 0 && !(exhausted && k_next >= 64)) {
-        if (k_next >= 64) {
-          int b = 0;
-          if (lane == 0) b = static_cast<int>(atomicAdd(&J.counters[6], 1ull));
-          b = __builtin_amdgcn_readfirstlane(b);
-          if (b >= num_batches) {
-            exhausted = true;
-            break;
-          }
-          const int tile = b / J.chunks;
-          bc = J.chunk_begin + (b - tile * J.chunks);
-          const int ty = tile / J.tiles_x;
-          bx = (tile - ty * J.tiles_x) << J.tile_lw;
-          by = ty << (6 - J.tile_lw);
-          k_next = 0;
-        }
-        const int take = min(min(__popcll(want), 64 - k_next), budget);
-        const int rank = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-            static_cast<uint32_t>(want >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(want), 0u)));
-        bool got = false;
-        if (!has() && rank < take) {
-          const int k = k_next + rank;
-          const int i = bx + (k & ((1 << J.tile_lw) - 1));
-          const int lr = by + (k >> J.tile_lw);
-          if (i < C.width && lr < J.row_count) {
-            u.px = static_cast<uint32_t>(i) | (static_cast<uint32_t>(lr) << 16);
-            u.chunk = bc;
-            u.sample = bc * J.chunk_samples;
-            u.s_end = min(u.sample + J.chunk_samples, C.spp);
-            u.acc = v3(0.0f, 0.0f, 0.0f);
-            fresh = true;
-            got = true;
-          }
-        }
-        const int n = __popcll(ballot(got));
-        started += n;
-        budget -= n;
-        k_next += take;
-        want = ballot(!has());
-      }
-      if (started != 0 && lane == 0)
-        __hip_atomic_fetch_add(Q.ctl + 5, static_cast<uint32_t>(started), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (exhausted && k_next >= 64 && !reported) {  // this wave hands out no more units
-      reported = true;
-      if (lane == 0) __hip_atomic_fetch_add(Q.ctl + 6, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (fresh) start_pixel_sample(u.ps, C, J, u.px, static_cast<uint32_t>(u.sample));
-    if (fresh || arrived) {
-      trav_begin(tr, S, u.ps.o, u.ps.d, u.ps.origin);
-      if (S.occluder >= 0) {
-        const float4* sp4 = S.spheres + static_cast<int64_t>(S.occluder) * S.sphere_f4;
-        if (COUNT) w.cnt.prim += 1;
-        const float th = sphere_t(sp4[0], sp4[1], u.ps.o, u.ps.d, tr.a, tr.inv_a, u.ps.time, kTMin, tr.tbest,
-                                  S.occluder == u.ps.origin);
-        if (th > 0.0f) {
-          tr.tbest = th;
-          tr.best = S.occluder;
-        }
-      }
-    }
-    fresh = arrived = false;
-    const uint64_t has_m = ballot(has());
-    const bool stalled = has_m != 0 && backlog != 0 && ballot(trav_active(tr)) == 0;  // shade queue full
-    if (has_m == 0 || stalled) {  // nothing to trace: done, or wait for the shading wave
-      if (has_m == 0 && reported && q_ld(Q.ctl + 5) == 0u) return;
-      __builtin_amdgcn_s_sleep(4);
-      if (++idle > (1u << 24)) {
-        const uint32_t own = static_cast<uint32_t>(__popcll(has_m));
-        if (lane == 0) q_timeout(J, Q.ctl, stalled ? 5u : 4u, own);
-        return;
-      }
-      continue;
-    }
-    idle = 0;
-    // 3. trips until q_deposit lanes have finished (or no lane traverses)
-    __builtin_amdgcn_s_setprio(1);
-    for (;;) {
-      const int at_leaf = __popcll(ballot(tr.todo < 0));
-      const bool inner_left = ballot(at_inner(tr)) != 0;
-      const bool leaf_trip = at_leaf >= J.leaf_batch || !inner_left;
-      if (leaf_trip && tr.todo < 0)
-        leaf_step<Stk, COUNT, false, false>(tr, S, u.ps.o, u.ps.d, u.ps.time, stk, w.cnt, w.corrupt);
-      if (at_inner(tr)) node_step4<Stk, COUNT, kGeomLds>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
-      const uint64_t trav = ballot(trav_active(tr));
-      const int ready = __popcll(ballot(!trav_active(tr)) & has_m) - backlog;
-      if (trav == 0 || ready >= J.q_deposit) break;
-    }
-    __builtin_amdgcn_s_setprio(0);
-  }
-}
-
-template <class Stk, bool COUNT, bool TEXF>
-__device__ __forceinline__ void render_stream_q(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                                const Stk& stk, WaveStats<COUNT>& w, lu32* qbase, int wave) {
-  RayQueues Q;
-  Q.S = J.q_shade;
-  Q.T = J.q_trace;
-  Q.ctl = qbase;
-  Q.sq = qbase + kQCtl;
-  Q.tq = Q.sq + kQEntryDw * Q.S;
-  if (wave >= J.q_tracers)
-    q_shader<COUNT, TEXF>(S, C, J, Q, w);
-  else
-    q_tracer<Stk, COUNT, TEXF>(S, C, J, stk, Q, w);
-}
-
 // Schedule 4: the same loop on a plain grid of 256-thread workgroups (scene read through the
 // caches; used when it does not fit in LDS). Waves take tiles from the same counter.
 template <int STACK, bool SPILL, bool COUNT, int WIDE, bool TEXF, bool RING>
@@ -2157,8 +1734,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 }
 
 // Schedule 3's body: the whole scene in the workgroup's LDS (render_kernel_lds with GEOM = kGeomLds).
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, bool QUEUE = false,
-          int PRIMS = kPrimsAny>
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCamera& C, const DevJob& J,
                                                  unsigned char* smem, int kFill, int wpb, uint64_t t0, int lane,
                                                  int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab) {
@@ -2202,8 +1778,6 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
     for (int k = threadIdx.x; k < S.num_perlins * 256; k += kFill) l_pvec[k] = S.perlin_vec[k];
     for (int k = threadIdx.x; k < S.num_perlins * 768; k += kFill) l_pperm[k] = S.perlin_perm[k];
   }
-  if (QUEUE && threadIdx.x < kQCtl)  // the ray queues start empty (RTG_RAY_QUEUE)
-    reinterpret_cast<uint32_t*>(smem + J.lds_queue)[threadIdx.x] = 0u;
   __syncthreads();
   DevScene L = S;
   L.nodes = l_nodes;
@@ -2234,10 +1808,6 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
     render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, stk, w, rtab);
-  } else if constexpr (QUEUE && STK16 && WIDE == 4 && !RING) {
-    lu32* qb = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_queue));
-    render_stream_q<LdsStack16<STACK>, COUNT, TEXF>(L, C, J, LdsStack16<STACK>{lstk16}, w, qb,
-                                                    __builtin_amdgcn_readfirstlane(wave));
   } else if constexpr (STK16) {
     render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack16<STACK>{lstk16}, w,
                                                                              rtab);
@@ -2258,20 +1828,14 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
 // persistent workgroups keep only the breadth-first top of the 4-wide tree in LDS (as many nodes as
 // fit beside the stacks, S.treelet_bytes); deeper nodes, primitives, materials and textures are read
 // through the caches. Every ray's first levels are then ds_reads instead of L1/L2 round trips.
-template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING, bool QUEUE = false,
+template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, int GEOM, bool RING,
           int PRIMS = kPrimsAny>
 // WAVES = 4: compiled for 5 waves per SIMD (<= 96 VGPRs) and launched with 4-wave workgroups (small
 // scenes, the dual launch's second workgroup) or 16-wave ones (book-1's main launch): one binary for
 // both shapes of the dual launch, and its 96-register budget runs the 16-wave workgroup faster than
 // the 104-register 16-wave build (dual -0.25 %, single -0.4 %, frames identical), so
 // the workgroup size is read at run time (kFill, wpb) instead of from WAVES.
-#ifdef RTG_AB_Q128
-// A/B build: the ray-queue kernel at 4 waves per SIMD (128 VGPRs, no scratch; the fifth workgroup of a CU
-// then starts only when one of the first four has finished, i.e. finds no work left)
-__global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 && !QUEUE ? 5 : 4)
-#else
 __global__ __launch_bounds__(WAVES == 4 ? 1024 : WAVES * 64, WAVES == 4 ? 5 : 4)
-#endif
 void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   const int kFill = WAVES == 4 ? static_cast<int>(blockDim.x) : WAVES * 64;  // threads of the workgroup
   const int wpb = kFill >> 6;                                                // waves of the workgroup
@@ -2307,7 +1871,7 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
     flush_stats<COUNT>(J, w, lane);
     trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
   } else {
-    render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, QUEUE, PRIMS>(S, C, J, smem, kFill, wpb, t0, lane, wave,
+    render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, PRIMS>(S, C, J, smem, kFill, wpb, t0, lane, wave,
                                                                           lstk, lstk16, rtab);
   }
 }
@@ -2458,11 +2022,11 @@ template <int STACK, bool SPILL, int WIDE, bool TEXF, int GEOM = kGeomLds, int W
 KernelChoice lds_kernel(bool count, bool ring, int threads = WAVES * 64) {
   KernelChoice k;
   k.fn = count ? reinterpret_cast<const void*>(
-                     &render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM, false, false, PRIMS>)
+                     &render_kernel_lds<STACK, SPILL, true, WAVES, WIDE, TEXF, GEOM, false, PRIMS>)
          : ring ? reinterpret_cast<const void*>(
-                      &render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, true, false, PRIMS>)
+                      &render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, true, PRIMS>)
                 : reinterpret_cast<const void*>(
-                      &render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, false, false, PRIMS>);
+                      &render_kernel_lds<STACK, SPILL, false, WAVES, WIDE, TEXF, GEOM, false, PRIMS>);
   k.block = threads;
   k.dynamic_lds = true;
   return k;
@@ -2550,16 +2114,6 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
     if (J.stack_esz != (stk16 ? 2 : 4)) return {};
     if (spill || (WIDE == 4 && !tex && !stk16))
       return tex ? lds_kernel<kLdsStack, true, WIDE, true>(count, ring) : lds_kernel<kLdsStack, true, WIDE, false>(count, ring);
-    if (WIDE == 4 && J.lds_queue >= 0 && stk16 && !ring) {  // the ray-queue prototype (4- or 16-wave workgroups)
-      KernelChoice k;
-      k.fn = count ? reinterpret_cast<const void*>(
-                         &render_kernel_lds<kLdsStack, false, true, 4, 4, false, kGeomLds, false, true>)
-                   : reinterpret_cast<const void*>(
-                         &render_kernel_lds<kLdsStack, false, false, 4, 4, false, kGeomLds, false, true>);
-      k.block = J.lds_waves * 64;
-      k.dynamic_lds = true;
-      return k;
-    }
     // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds),
     // one per primitive class (kPrimsAny...: the leaf test compiled for the scene's primitives only)
 #ifndef RTG_AB_PRIMS_ANY

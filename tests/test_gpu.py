@@ -643,37 +643,6 @@ def test_exact_t_ties_match_oracle(gpu_lib, oracle, bvh):
     assert n[GREEN] > 200 and n[BLUE] > 100 and n[RED] == 0 and n[WHITE] == 0, n
 
 
-@pytest.mark.parametrize("name,W,spp,depth", [("cornell_box", 64, 16, 100), ("cornell_box", 48, 40, 50),
-                                               ("quads", 64, 8, 50), ("checkered_spheres", 64, 8, 20),
-                                               ("bouncing_spheres", 96, 8, 30), ("bouncing_spheres", 64, 40, 50)])
-def test_ray_queue_matches_oracle(gpu_lib, scenes, oracle, monkeypatch, name, W, spp, depth):
-    """RTG_RAY_QUEUE=1 (the cross-wave prototype): rays move between the waves of a
-    workgroup through LDS queues (tracing waves and shading waves). A unit's samples stay in one
-    context, in order, so the frame and the segment count are cpu_ref32's and the per-wave schedule's,
-    bit for bit; 40 spp covers chunked units (partial sums in chunk order)."""
-    s = scenes.build(name, rand_seed=1)
-    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
-    c.image_width, c.samples_per_pixel, c.max_depth = W, spp, depth
-    ds0 = gpu_lib.scene_create(s.desc)
-    g0, st0 = ds0.render_host(c)
-    assert ds0.plan(c).ray_queue == 0
-    ds0.close()
-    monkeypatch.setenv("RTG_RAY_QUEUE", "1")
-    ds = gpu_lib.scene_create(s.desc)  # knobs are read once per scene
-    monkeypatch.delenv("RTG_RAY_QUEUE")
-    p = ds.plan(c)
-    # small scenes: five 4-wave workgroups per CU; book-1: one 16-wave workgroup (no dual launch)
-    assert p.ray_queue > 0 and p.schedule == 3 and p.dual == 0, p.as_dict()
-    assert p.waves_per_workgroup == (16 if name == "bouncing_spheres" else 4), p.as_dict()
-    g, st = ds.render_host(c)
-    gc, stc = ds.render_host(c, count=True)
-    ds.close()
-    o, segs = oracle.render_f32(s.desc, c)
-    assert_parity(g, o, st, segs)
-    assert np.array_equal(g, g0) and st.segments == st0.segments
-    assert np.array_equal(gc, g) and stc.segments == st.segments and stc.box_tests > 0
-
-
 def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypatch):
     """Deep BVHs keep the first stack entries in LDS and the rest in a global per-wave spill area
     (the 1M-sphere scene needs 36 entries). RTG_STACK_LDS_ENTRIES lowers the LDS part so that the

@@ -301,9 +301,9 @@ typedef struct rtg_launch_plan {
   int32_t treelet_visit_permille; /* treelet_hot: of the probe's node visits, the share (per mille)
                                      that the treelet_nodes in LDS take */
   /* round 4, layout-compatible (two of ABI 5's reserved words): */
-  int32_t ray_queue;         /* > 0: rays move between the waves of a workgroup through LDS queues (the
-                                RTG_RAY_QUEUE prototype; the shade queue's capacity), 0: off */
-  int32_t node_width;        /* BVH node width the kernels traverse: 2, 4, or 8 (RTG_BVH_WIDTH=8 A/B) */
+  int32_t ray_queue;         /* always 0 since round 5 (the RTG_RAY_QUEUE prototype was retired to
+                                tools/experiments/ray_queue.patch); the word keeps the layout */
+  int32_t node_width;        /* BVH node width the kernels traverse: 2 (RTG_BVH_MEDIAN) or 4 */
   int32_t reserved_[1];
 } rtg_launch_plan;
 

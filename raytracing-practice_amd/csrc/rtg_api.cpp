@@ -289,66 +289,9 @@ bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
   std::vector<int> bad(host_threads(nn), 0);  // 1: a node without children, 2: a leaf not encodable
   host_par_for(nn, [&](int64_t b, int64_t e, int th) {
     for (int64_t k = b; k < e && !bad[th]; ++k) {
-      const BuildNodeW<W>& n0 = t.nodes[k];
-#ifdef RTG_AB_W8_OCT
-      // A/B: octant-ordered child slots (Ylitie et al. 2017): slot s holds the child met first by rays of
-      // direction-sign octant s (bit a set: axis a negative), assigned greedily by dot(centre offset, octant)
-      BuildNodeW<W> n = n0;
-      constexpr double kInfD = std::numeric_limits<double>::infinity();
-      if (W == 8) {
-        double P[3] = {0, 0, 0};
-        int nc = 0;
-        for (int c = 0; c < W; ++c)
-          if (n0.child[c] != kEmptyChild) {
-            ++nc;
-            for (int a = 0; a < 3; ++a) P[a] += 0.5 * (n0.lo[c][a] + n0.hi[c][a]);
-          }
-        for (int a = 0; a < 3; ++a) P[a] /= nc;
-        struct Pair {
-          double cost;
-          int c, s;
-        };
-        std::vector<Pair> pairs;
-        for (int c = 0; c < W; ++c) {
-          if (n0.child[c] == kEmptyChild) continue;
-          for (int sl = 0; sl < W; ++sl) {
-            double cst = 0.0;
-            for (int a = 0; a < 3; ++a)
-              cst += (0.5 * (n0.lo[c][a] + n0.hi[c][a]) - P[a]) * ((sl >> a) & 1 ? -1.0 : 1.0);
-            pairs.push_back({cst, c, sl});
-          }
-        }
-        std::stable_sort(pairs.begin(), pairs.end(), [](const Pair& x, const Pair& y) { return x.cost < y.cost; });
-        int slot_of[W], child_in[W];
-        std::fill(slot_of, slot_of + W, -1);
-        std::fill(child_in, child_in + W, -1);
-        for (const Pair& q : pairs)
-          if (slot_of[q.c] < 0 && child_in[q.s] < 0) slot_of[q.c] = q.s, child_in[q.s] = q.c;
-        for (int sl = 0; sl < W; ++sl) {
-          const int c = child_in[sl];
-          n.child[sl] = c >= 0 ? n0.child[c] : kEmptyChild;
-          n.count[sl] = c >= 0 ? n0.count[c] : 0;
-          for (int a = 0; a < 3; ++a) {
-            n.lo[sl][a] = c >= 0 ? n0.lo[c][a] : kInfD;
-            n.hi[sl][a] = c >= 0 ? n0.hi[c][a] : -kInfD;
-          }
-        }
-        if (n.child[0] == kEmptyChild) {  // slot 0 must be a child (the empty-node check below)
-          for (int sl = 1; sl < W; ++sl)
-            if (n.child[sl] != kEmptyChild) {
-              std::swap(n.child[0], n.child[sl]);
-              std::swap(n.count[0], n.count[sl]);
-              std::swap(n.lo[0], n.lo[sl]);
-              std::swap(n.hi[0], n.hi[sl]);
-              break;
-            }
-        }
-      }
-#else
-      const BuildNodeW<W>& n = n0;
-#endif
+      const BuildNodeW<W>& n = t.nodes[k];
       float* f = &out->nodes[k * kWords];
-      if (n0.child[0] == kEmptyChild) {
+      if (n.child[0] == kEmptyChild) {
         bad[th] = 1;
         break;
       }
@@ -501,7 +444,6 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   out->stack_need = bvh.depth;
   out->node_width = 2;
   Bvh4 bvh4;
-  Bvh8 bvh8;
   if (gpu_bvh) {
     out->gpu_bvh = true;
     out->node_width = 4;
@@ -526,34 +468,14 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         cp.max_leaf = std::min(8, std::max(1, ml));
       }
     }
-    // RTG_BVH_WIDTH=8 (A/B): 8-wide nodes for the cache-read schedules, traversed with
-    // one stack entry per node (the node and its hit children not yet visited), so the stack holds at
-    // most one entry per tree level
-    const char* wenv = std::getenv("RTG_BVH_WIDTH");
-    if (wenv && std::atoi(wenv) == 8) {
-      collapse_bvh<8>(bvh, &bvh8, cp);
-      phase("collapse");
-      // a stack entry packs the node's byte offset / 32 into 24 bits beside the 8-bit child mask
-      if (static_cast<int64_t>(bvh8.nodes.size()) * node_bytes(8) >= (int64_t(1) << 29)) {
-        *err = "8-wide BVH too large for its stack entries (RTG_BVH_WIDTH=8)";
-        return false;
-      }
-      reorder_top_bfs(&bvh8, kTreeletBfsNodes);
-      phase("bfs");
-      out->num_nodes = static_cast<int64_t>(bvh8.nodes.size());
-      out->depth = bvh8.depth;
-      out->stack_need = bvh8.depth;
-      out->node_width = 8;
-    } else {
-      collapse_bvh4(bvh, &bvh4, cp);
-      phase("collapse");
-      reorder_top_bfs(&bvh4, kTreeletBfsNodes);
-      phase("bfs");
-      out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
-      out->depth = bvh4.depth;
-      out->stack_need = bvh4.max_pushes;
-      out->node_width = 4;
-    }
+    collapse_bvh4(bvh, &bvh4, cp);
+    phase("collapse");
+    reorder_top_bfs(&bvh4, kTreeletBfsNodes);
+    phase("bfs");
+    out->num_nodes = static_cast<int64_t>(bvh4.nodes.size());
+    out->depth = bvh4.depth;
+    out->stack_need = bvh4.max_pushes;
+    out->node_width = 4;
   }
   if (std::getenv("RTG_VERBOSE"))
     std::fprintf(stderr, "[rtg] bvh: %lld primitives, %zu binary nodes -> %lld nodes of width %d, depth %d, stack %d\n",
@@ -622,7 +544,6 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   phase("prims");
   // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
   if (out->node_width == 4 && !emit_wide(bvh4, out, err)) return false;
-  if (out->node_width == 8 && !emit_wide(bvh8, out, err)) return false;
   // child-pair nodes: 64 B
   if (out->node_width == 2) out->nodes.resize(bvh.nodes.size() * 16);
   for (size_t k = 0; out->node_width == 2 && k < bvh.nodes.size(); ++k) {
@@ -1028,7 +949,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
   s->dev.treelet_bytes = 0;  // set per render by the treelet schedule
   s->dev.treelet_lds = 0;
   s->dev.node_limit = static_cast<int32_t>(
-      std::min<int64_t>(hs.num_nodes * node_bytes(hs.node_width == 8 ? 8 : 4), INT32_MAX));
+      std::min<int64_t>(hs.num_nodes * node_bytes(4), INT32_MAX));
   s->dev.num_refs = static_cast<int64_t>(hs.refs.size());
   s->dev.num_spheres = static_cast<int64_t>(hs.spheres.size() / 8);
   s->dev.num_quads = static_cast<int64_t>(hs.quads.size() / 20);

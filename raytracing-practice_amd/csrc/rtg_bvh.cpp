@@ -809,7 +809,6 @@ void collapse_bvh(const Bvh& bin, BvhW<W>* out, const CollapseParams& prm) {
   rec.fill(0, 0, 1, 0);
 }
 template void collapse_bvh<4>(const Bvh&, BvhW<4>*, const CollapseParams&);
-template void collapse_bvh<8>(const Bvh&, BvhW<8>*, const CollapseParams&);
 
 template <int W>
 void reorder_top_bfs(BvhW<W>* t, int64_t top) {
@@ -843,7 +842,6 @@ void reorder_top_bfs(BvhW<W>* t, int64_t top) {
   t->nodes.swap(out);
 }
 template void reorder_top_bfs<4>(BvhW<4>*, int64_t);
-template void reorder_top_bfs<8>(BvhW<8>*, int64_t);
 
 void hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
   const int64_t words = 7 * width, bytes = 28 * width;  // a node: 6 plane rows + 1 code row of `width`

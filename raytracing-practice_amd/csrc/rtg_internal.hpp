@@ -74,7 +74,6 @@ struct BuildNodeW {
   int32_t count[W];
 };
 using BuildNode4 = BuildNodeW<4>;
-using BuildNode8 = BuildNodeW<8>;
 
 template <int W>
 struct BvhW {
@@ -83,7 +82,6 @@ struct BvhW {
   int32_t max_pushes = 0;  // most stack entries an ordered traversal (one per sibling) can hold at once
 };
 using Bvh4 = BvhW<4>;
-using Bvh8 = BvhW<8>;
 
 // Collapse a binary child-pair BVH into a W-wide one: greedy (open the largest-area inner child until
 // W slots are filled; leaves unchanged) or SAH-optimal (dynamic program over the binary tree; may

@@ -335,8 +335,8 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
   t.ix = __builtin_amdgcn_rcpf(d.x);
   t.iy = __builtin_amdgcn_rcpf(d.y);
   t.iz = __builtin_amdgcn_rcpf(d.z);
-  // byte offset of the far-plane rows (hi.x after lo.x, ...): 48 in 4-wide nodes, 96 in 8-wide ones
-  constexpr int32_t kHalf = WIDE == 8 ? 96 : 48;
+  // byte offset of the far-plane rows (hi.x after lo.x, ...) in 4-wide nodes
+  constexpr int32_t kHalf = 48;
   t.sx = (static_cast<uint32_t>(ibits(t.ix)) >> 31) * kHalf;
   t.sy = (static_cast<uint32_t>(ibits(t.iy)) >> 31) * kHalf;
   t.sz = (static_cast<uint32_t>(ibits(t.iz)) >> 31) * kHalf;
@@ -608,140 +608,13 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
-// ---- 8-wide nodes (RTG_BVH_WIDTH=8, the cache-read schedules; A/B of DESIGN.md §8) ----
-// Node: 224 B, rows of eight floats lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, then eight int32 codes (+192).
-// A visit tests all eight child boxes, continues with the nearest hit child and pushes ONE stack entry
-// for the rest: the node's byte offset / 32 (node offsets are multiples of 224 = 7 x 32) in the upper 24
-// bits and the 8-bit mask of its hit children not yet visited; a pop takes the lowest slot of the top
-// entry (slot order: the far children are not sorted, which r03 measured at +0.5 % box tests on 4-wide
-// nodes) and reads that child's code. The stack then holds at most one entry per tree level (config 5:
-// the tree's depth instead of the 36 sibling entries of the sorted 4-wide pushes, so no spill).
-constexpr int32_t kNode8Bytes = 224;
-
-template <int GEOM>
-__device__ __forceinline__ int32_t code8(const DevScene& S, int32_t node, int slot) {
-  if (GEOM == kGeomTreelet && node < S.treelet_bytes) return lds_ld1(S.treelet_lds + node + 192 + 4 * slot);
-  return *reinterpret_cast<const int32_t*>(reinterpret_cast<const char*>(S.nodes) + node + 192 + 4 * slot);
-}
-
-#ifdef RTG_AB_W8_OCT
-// the ray's direction-sign octant (bit a: axis a negative), from the far-plane row offsets (0 or 96)
-__device__ __forceinline__ int oct8(const Trav& t) {
-  return (t.sx != 0 ? 1 : 0) | (t.sy != 0 ? 2 : 0) | (t.sz != 0 ? 4 : 0);
-}
-#endif
-
-template <class Stk, int GEOM>
-__device__ __forceinline__ void trav_pop8(Trav& t, const DevScene& S, const Stk& stk) {
-  if (t.sp == 0) {
-    t.todo = kTravDone;
-    return;
-  }
-  const int32_t g = stk.load(t.sp - 1);
-  uint32_t m = static_cast<uint32_t>(g) & 255u;
-  const int32_t node = static_cast<int32_t>(static_cast<uint32_t>(g) >> 8) << 5;
-  const int p = __builtin_ctz(m);
-  m &= m - 1u;
-  if (m != 0u)
-    stk.store(t.sp - 1, (g & ~255) | static_cast<int32_t>(m));
-  else
-    --t.sp;
-#ifdef RTG_AB_W8_OCT  // the entry's mask is in octant order: position p is slot p ^ octant
-  t.todo = code8<GEOM>(S, node, p ^ oct8(t));
-#else
-  t.todo = code8<GEOM>(S, node, p);
-#endif
-}
-
-template <class Stk, bool COUNT, int GEOM>
-__device__ __forceinline__ void node_step8(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
-                                           bool& overflow, bool& corrupt) {
-  if (t.todo >= S.node_limit) {  // corrupt child code: report, never read out of bounds
-    corrupt = true;
-    t.todo = kTravDone;
-    return;
-  }
-  if (COUNT && S.node_visits) atomicAdd(S.node_visits + t.todo / kNode8Bytes, 1u);
-  const int32_t sx = t.sx, sy = t.sy, sz = t.sz;
-  const uint32_t na = static_cast<uint32_t>(t.todo);
-  const char* nb = reinterpret_cast<const char*>(S.nodes) + t.todo;
-  nf4 r[12];  // near x, y, z then far x, y, z; two halves (children 0-3, 4-7) each
-  const int32_t off[6] = {sx, 32 + sy, 64 + sz, 96 - sx, 128 - sy, 160 - sz};
-  if (GEOM == kGeomTreelet && t.todo < S.treelet_bytes) {
-    const uint32_t la = S.treelet_lds + na;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      r[2 * k] = lds_ld4(la + off[k]);
-      r[2 * k + 1] = lds_ld4(la + off[k] + 16);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      r[2 * k] = *reinterpret_cast<const nf4*>(nb + off[k]);
-      r[2 * k + 1] = *reinterpret_cast<const nf4*>(nb + off[k] + 16);
-    }
-  }
-  if (COUNT) cnt.box += 8;
-  const f2 ix = {t.ix, t.ix}, iy = {t.iy, t.iy}, iz = {t.iz, t.iz};
-  const f2 ox = {t.ox, t.ox}, oy = {t.oy, t.oy}, oz = {t.oz, t.oz};
-  // the eight children's entry / exit distances (sign-selected slab planes, as node_step4), keys of
-  // the hit ones (entry distance bits, slot in the low 3 bits) and the hit mask
-  uint32_t mask = 0u, kmin = ~0u;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const nf4 nx = r[h], ny = r[2 + h], nz = r[4 + h], fx = r[6 + h], fy = r[8 + h], fz = r[10 + h];
-    const f2 n_x[2] = {pk_fma(f2{nx.x, nx.y}, ix, ox), pk_fma(f2{nx.z, nx.w}, ix, ox)};
-    const f2 n_y[2] = {pk_fma(f2{ny.x, ny.y}, iy, oy), pk_fma(f2{ny.z, ny.w}, iy, oy)};
-    const f2 n_z[2] = {pk_fma(f2{nz.x, nz.y}, iz, oz), pk_fma(f2{nz.z, nz.w}, iz, oz)};
-    const f2 f_x[2] = {pk_fma(f2{fx.x, fx.y}, ix, ox), pk_fma(f2{fx.z, fx.w}, ix, ox)};
-    const f2 f_y[2] = {pk_fma(f2{fy.x, fy.y}, iy, oy), pk_fma(f2{fy.z, fy.w}, iy, oy)};
-    const f2 f_z[2] = {pk_fma(f2{fz.x, fz.y}, iz, oz), pk_fma(f2{fz.z, fz.w}, iz, oz)};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int p = c >> 1, e = c & 1;
-      const float tn = fmaxf(fmaxf(fmaxf(n_x[p][e], n_y[p][e]), n_z[p][e]), kTMin);
-      const float tf = fminf(fminf(fminf(f_x[p][e], f_y[p][e]), f_z[p][e]), t.tbest);
-      const uint32_t slot = 4u * h + c;
-      const bool hit = tn <= tf;
-      mask |= hit ? (1u << slot) : 0u;
-      kmin = min(kmin, hit ? ((static_cast<uint32_t>(ibits(tn)) & ~7u) | slot) : ~0u);
-    }
-  }
-  if (kmin == ~0u) {
-    trav_pop8<Stk, GEOM>(t, S, stk);
-    return;
-  }
-  const int slot = static_cast<int>(kmin & 7u);
-  mask &= ~(1u << slot);
-#ifdef RTG_AB_W8_OCT  // the other hit children in octant order (bit p = slot p ^ octant): XOR the bit index
-  {
-    const int o = oct8(t);
-    if (o & 1) mask = ((mask & 0x55u) << 1) | ((mask >> 1) & 0x55u);
-    if (o & 2) mask = ((mask & 0x33u) << 2) | ((mask >> 2) & 0x33u);
-    if (o & 4) mask = ((mask & 0x0fu) << 4) | ((mask >> 4) & 0x0fu);
-  }
-#endif
-  if (mask != 0u) {  // one entry for the node's other hit children
-    if (t.sp < stk.capacity())
-      stk.store(t.sp++, ((t.todo >> 5) << 8) | static_cast<int32_t>(mask));
-    else
-      overflow = true;
-  }
-  t.todo = code8<GEOM>(S, t.todo, slot);
-}
-
 // Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
 // LDS schedule outside the COUNT diagnostics, as for node codes).
 template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,
           int PRIMS = kPrimsAny>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
-  auto pop = [&]() {
-    if constexpr (WIDE == 8)
-      trav_pop8<Stk, GEOM>(t, S, stk);
-    else
-      trav_pop(t, stk);
-  };
+  auto pop = [&]() { trav_pop(t, stk); };
   const int32_t code = ~t.todo;
   const int32_t first = code >> 3;
   const int32_t count = (code & 7) + 1;
@@ -1618,19 +1491,11 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
       // overhead, and a lane's second step overlaps the other lanes' load latency), 1 for LDS scenes
       // (2: neutral, 3: +3 %)
-#ifndef RTG_AB_CACHE_NODE_REPS
-#define RTG_AB_CACHE_NODE_REPS 2
-#endif
-#ifndef RTG_AB_NODE8_REPS
-#define RTG_AB_NODE8_REPS 1
-#endif
-      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : (WIDE == 8 ? RTG_AB_NODE8_REPS : RTG_AB_CACHE_NODE_REPS);
+      constexpr int kNodeReps = GEOM == kGeomLds ? 1 : 2;
 #pragma unroll
       for (int rep = 0; rep < kNodeReps; ++rep) {
         if (at_inner(tr)) {
-          if constexpr (WIDE == 8)
-            node_step8<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
-          else if constexpr (WIDE == 4)
+          if constexpr (WIDE == 4)
             node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
           else
             node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
@@ -2077,11 +1942,6 @@ KernelChoice legacy_kernel(bool count, int variant) {
 KernelChoice treelet_kernel(const DevScene& S, const DevJob& J, bool count) {
   if (J.lds_stack > kLdsStack || J.stack_esz != 4 || J.lds_waves != kLdsWaves) return {};
   const bool spill = J.spill_depth > 0, tex = S.tex_full != 0, ring = J.ring_log2 >= 0 && !count;
-  if (S.node_width == 8) {  // A/B (RTG_BVH_WIDTH=8): scenes without image / noise textures
-    if (tex) return {};
-    return spill ? lds_kernel<kLdsStack, true, 8, false, kGeomTreelet>(count, ring)
-                 : lds_kernel<kLdsStack, false, 8, false, kGeomTreelet>(count, ring);
-  }
   if (S.node_width != 4) return {};
   // sphere-only scenes (the 1M field) get a build without the quad test (kPrimsSpheres, as default_kernel)
 #ifndef RTG_AB_PRIMS_ANY
@@ -2146,7 +2006,6 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
 // The kernel a render of this plan runs (fn == nullptr: no kernel fits the plan).
 KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool count, int variant) {
   if (variant == 5) return treelet_kernel(S, J, count);
-  if (S.node_width == 8) return {};  // 8-wide trees: the treelet schedule only (A/B)
   if (variant == 3 || variant == 0)
     return S.node_width == 4 ? default_kernel<4>(S, J, count, stack, variant == 3)
                              : default_kernel<2>(S, J, count, stack, variant == 3);
@@ -2207,7 +2066,6 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   // the node array first (at LDS address 0: inner-node codes are its byte offsets, <= 15 bits for
   // trees of <= 292 4-wide nodes, LdsStack16), then the traversal stacks (esz bytes per entry)
   const int64_t nodes = 0;
-  if (S.node_width == 8) return -1;  // 8-wide trees: the treelet schedule only (A/B)
   int64_t off = a16(S.num_nodes * (S.node_width == 4 ? 112 : 64));
   const int64_t stacks = off;
   off = a16(off + int64_t(waves) * stack * 64 * esz);

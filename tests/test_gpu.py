@@ -138,32 +138,6 @@ def test_bvh_mode_does_not_change_the_image(gpu_lib, scenes):
     assert np.array_equal(imgs[0], imgs[1])
 
 
-@pytest.mark.parametrize("name,grid,W", [("bouncing_spheres", 11, 96), ("bouncing_spheres", 500, 128),
-                                         ("cornell_box", 0, 64)])
-def test_wide8_nodes_match_oracle(gpu_lib, scenes, oracle, monkeypatch, name, grid, W):
-    """RTG_BVH_WIDTH=8 (the A/B of DESIGN.md §8): 8-wide nodes on the treelet schedule, one stack entry
-    per visited node (node + mask of its hit children not yet visited). The frame and the segment count
-    are the oracle's and the 4-wide tree's, bit for bit; the 8-wide tree's stack needs no spill."""
-    s = scenes.build(name, grid=grid, rand_seed=1)
-    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
-    c.image_width, c.aspect_ratio, c.samples_per_pixel, c.max_depth = W, 16.0 / 9.0, 4, 30
-    ds4 = gpu_lib.scene_create(s.desc)
-    g4, st4 = ds4.render_host(c)
-    ds4.close()
-    monkeypatch.setenv("RTG_BVH_WIDTH", "8")
-    ds = gpu_lib.scene_create(s.desc)  # the host compile reads the knob
-    monkeypatch.delenv("RTG_BVH_WIDTH")
-    p = ds.plan(c)
-    assert p.schedule == 5 and p.spill_entries == 0 and p.treelet_nodes > 0, p.as_dict()
-    g, st = ds.render_host(c)
-    gc, stc = ds.render_host(c, count=True)  # the counting build: same frame, no overflow / corrupt code
-    ds.close()
-    o, segs = oracle.render_f32(s.desc, c)
-    assert_parity(g, o, st, segs)
-    assert np.array_equal(g, g4) and st.segments == st4.segments
-    assert np.array_equal(gc, g) and stc.box_tests > 0 and stc.box_tests % 8 == 0
-
-
 def test_schedules_give_identical_frames(gpu_lib, scenes):
     """All kernel schedules (persistent LDS-resident default, plain-grid ballot-batched,
     per-segment, the first kernel) differ only in when a lane's work runs, never in what it

@@ -155,12 +155,12 @@ typedef struct rtg_camera_params {
 #define RTG_RENDER_COUNT 0x4      /* also count box / primitive tests (slower, diagnostic) */
 /* Diagnostic schedule selection (A/B of kernel variants; 0 = the default everywhere):
  * bits 8-15 schedule (0 default = 3 when the scene geometry fits in LDS, else 5 for 4-wide trees,
- * else 4; 1 one closest-hit query per loop trip; 2 the first kernel (1 and 2 need a binary BVH:
- * RTG_BVH_MEDIAN); 3 persistent workgroups with LDS-resident geometry (five 4-wave workgroups per
+ * else 4; 3 persistent workgroups with LDS-resident geometry (five 4-wave workgroups per
  * CU for small scenes, else a 16-wave one plus, where it fits, a second launch of one 4-wave
  * workgroup per CU: 5 waves per SIMD); 4 ballot-batched on
  * a plain grid, scene through the caches; 5 the persistent workgroups with the breadth-first top
- * of a 4-wide tree in LDS and the rest through the caches),
+ * of a 4-wide tree in LDS and the rest through the caches; round 1's per-segment schedules 1 and 2
+ * were retired in round 5 and return RTG_E_UNSUPPORTED),
  * bits 16-23 shade batch of schedule 0 in 64ths of the live lanes (0 = library default). */
 #define RTG_RENDER_SCHEDULE(n) (((n) & 0xff) << 8)
 #define RTG_RENDER_SHADE_BATCH(n) (((n) & 0xff) << 16)
@@ -271,7 +271,7 @@ rtg_status rtg_render_wait(rtg_scene* scene, rtg_render_stats* stats);
  * the real VGPR count, not a profiler's allocation granule). The bench record reports it beside the
  * roofline so the counted occupancy and the kernel that was timed are named by the library itself. */
 typedef struct rtg_launch_plan {
-  int32_t schedule;          /* 3 LDS-resident scene, 5 LDS treelet, 0 plain grid, 1/2 A/B kernels */
+  int32_t schedule;          /* 3 LDS-resident scene, 5 LDS treelet, 0 plain grid */
   int32_t workgroups;        /* main launch */
   int32_t waves_per_workgroup;
   int32_t lds_bytes;         /* dynamic LDS per workgroup of the main launch */

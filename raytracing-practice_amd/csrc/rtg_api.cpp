@@ -20,7 +20,6 @@
 #include "rtg_internal.hpp"
 
 namespace rtg {
-int kernel_stack_depth(int bvh_depth);
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,
                           hipStream_t stream);
 KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool count, int variant);
@@ -229,8 +228,6 @@ Knobs read_knobs() {
   int w = 0;
   if (num("RTG_LDS_WAVES", 4, 16, &w) && (w == 4 || w == 16)) k.lds_waves = w;
   num("RTG_DUAL", 0, 1, &k.dual);
-  int st = 0;
-  if (num("RTG_STACK", 16, 64, &st) && (st == 16 || st == 32 || st == 64)) k.stack = st;
   int ts = 0;  // tile-ring slots: 0 or a power of two (tests shrink the ring to force slot waits)
   if (num("RTG_TILE_SLOTS", 0, 65536, &ts) && (ts & (ts - 1)) == 0) k.tile_slots = ts;
   num("RTG_TREELET_STACK", 4, 16, &k.treelet_stack);
@@ -1185,8 +1182,7 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   // schedule: explicit (diagnostic flags) or the persistent LDS kernel when the geometry fits
   int variant = (job->flags >> 8) & 0xff;
   // traversal stack: 16 LDS entries for the persistent kernel, 16 or 32 for the plain grid (the
-  // most its occupancy allows), deeper BVHs spill the rest to a global per-wave area; the A/B
-  // schedules 1 and 2 keep the whole stack in LDS.
+  // most its occupancy allows), deeper BVHs spill the rest to a global per-wave area
   const int need = std::max(1, s->stack_need);
   int treelet_entries = kLdsStack;  // LDS stack entries per lane of the treelet schedule
   DevScene& dscene = P->dscene;
@@ -1260,8 +1256,9 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     dj.shade_batch = (variant == 5 || variant == 0) ? kCacheShadeBatch
                                                     : (s->dev.tex_full ? kTexShadeBatch : kDefaultShadeBatch);
   if (variant == 3 && lds_bytes < 0) return fail(RTG_E_INVALID, "scene does not fit the LDS schedule");
-  if ((variant == 1 || variant == 2) && s->dev.node_width != 2)
-    return fail(RTG_E_INVALID, "schedules 1 and 2 need a binary BVH (RTG_BVH_MEDIAN)");
+  // schedules 1 and 2 (round 1's per-segment kernels) were retired in round 5
+  // (tools/experiments/legacy_schedules.patch)
+  if (variant == 1 || variant == 2) return fail(RTG_E_UNSUPPORTED, "schedules 1 and 2 were retired (round 5)");
   if (variant < 0 || variant > 5) return fail(RTG_E_INVALID, "unknown render schedule");
   int stack_depth = 0;
   int grid_blocks = 1, grid_waves = 0;
@@ -1273,11 +1270,7 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     stack_depth = need <= 16 ? 16 : 32;
     grid_blocks = std::max(1, std::min(s->num_cus * kPlainWgsPerCu, (dj.num_tiles + 3) / 4));
     grid_waves = grid_blocks * 4;
-  } else {
-    stack_depth = kernel_stack_depth(need);
-    if (stack_depth < 0) return fail(RTG_E_UNSUPPORTED, "schedules 1 and 2 support BVH stacks up to 64");
   }
-  if (K.stack > 0) stack_depth = K.stack;  // experiments only
   dj.lds_stack = stack_depth;
   // RTG_STACK_LDS_ENTRIES (tests): keep fewer entries in LDS so the global spill path is exercised
   if (lds_entries_knob) dj.lds_stack = std::min(stack_depth, K.stack_lds_entries);
@@ -1306,10 +1299,6 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     dj.ring_log2 = lg;
     P->ring_slots = 1 << lg;
     P->ring_bytes = (static_cast<size_t>(dj.chunks) << (lg + 10)) + (size_t(8) << lg);
-  }
-  if (!P->default_sched) {  // schedules 1 and 2 keep one running sum per pixel
-    dj.chunks = 1;
-    dj.chunk_samples = std::max(1, cam->samples_per_pixel);
   }
   P->skip_kernel = P->progressive && dc.max_depth <= 0;  // every chunk sum is black
   if (P->skip_kernel || variant != 3) lds4 = -1;
@@ -1464,7 +1453,7 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
   if (st != RTG_OK) return st;
   *out = rtg_launch_plan{};
   out->schedule = P.variant;
-  out->workgroups = P.variant == 1 || P.variant == 2 ? ((P.W + 15) / 16) * ((P.rows + 15) / 16) : P.grid_blocks;
+  out->workgroups = P.grid_blocks;
   out->waves_per_workgroup = P.kmain.block / 64;
   out->lds_bytes = P.kmain.dynamic_lds ? P.lds_bytes : 0;
   const KernelResources r = kernel_resources(P.kmain.fn);
@@ -1588,7 +1577,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   const bool trace = !K.wave_trace.empty();
   int64_t trace_slots = 0;
   if (trace) {
-    trace_slots = P.default_sched ? int64_t(P.grid_waves) : int64_t((W + 15) / 16) * ((rows + 15) / 16) * 4;
+    trace_slots = int64_t(P.grid_waves);
     RTG_HIP(hipMallocAsync(scratch.add(), trace_slots * 32, stream), "hipMalloc(trace)");
     dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");

@@ -191,7 +191,6 @@ struct KernelChoice {
   const void* fn = nullptr;
   int block = 0;             // threads per workgroup
   bool dynamic_lds = false;  // persistent kernels: the plan's LDS bytes are dynamic shared memory
-  bool grid2d = false;       // A/B schedules 1 and 2: one 16x16-pixel workgroup per tile
 };
 struct KernelResources {
   bool ok = false;
@@ -237,7 +236,6 @@ struct Knobs {
   int stack_lds_entries = 0;    // RTG_STACK_LDS_ENTRIES 1..32 (tests: exercise the global spill)
   int lds_waves = 0;            // RTG_LDS_WAVES 4 | 16 (0: by scene size)
   int dual = -1;                // RTG_DUAL 0 | 1 (-1: where it fits)
-  int stack = 0;                // RTG_STACK 16 | 32 | 64 (A/B schedules only)
   int tile_slots = -1;          // RTG_TILE_SLOTS 0 (full-frame partials) | 1..65536 (-1: by chunks)
   int treelet_stack = 16;       // RTG_TREELET_STACK 4..16: LDS stack entries of the treelet schedule
                                 // (fewer: more treelet nodes, more spill traffic; spilling trees only)

@@ -677,113 +677,6 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
   pop();
 }
 
-// One unit of traversal work for this lane (used by the per-segment schedule).
-template <class Stk, bool COUNT>
-__device__ __forceinline__ void trav_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
-                                          const Stk& stk, Counts<COUNT>& cnt, bool& overflow,
-                                          bool& corrupt) {
-  if (t.todo >= 0)
-    node_step<Stk, COUNT>(t, S, stk, cnt, overflow, corrupt);
-  else
-    leaf_step<Stk, COUNT>(t, S, o, d, time, stk, cnt, corrupt);
-}
-
-// Schedule 2: the first kernel's monolithic closest-hit loop (kept for A/B).
-// Closest hit over the child-pair BVH (replaces hittable_list::hit -> bvh_node::hit ->
-// aabb::hit, hittable_list.hpp:40-64, bvh_node.hpp:80-94, aabb.hpp:61-112). Ordered
-// traversal: the nearer child first, the farther pushed on the lane's LDS stack.
-template <int STACK, bool COUNT>
-__device__ __forceinline__ int32_t closest_hit(const DevScene& S, V3 o, V3 d, float time, int32_t origin,
-                                               float& tbest, int32_t* stk, Counts<COUNT>& cnt,
-                                               bool& overflow, bool& corrupt) {
-  int32_t best = -1;
-  if (S.num_nodes == 0) return best;
-  const V3 inv = v3(__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y),
-                    __builtin_amdgcn_rcpf(d.z));
-  const V3 oi = v3(-o.x * inv.x, -o.y * inv.y, -o.z * inv.z);
-  const float a = dot(d, d), inv_a = div_rn(1.0f, a);
-  int sp = 0;
-  int32_t todo = 0;
-  while (true) {
-    if (todo >= 0) {
-      if (todo >= S.num_nodes) {  // corrupt child code: report, never read out of bounds
-        corrupt = true;
-        break;
-      }
-      const float4* n = S.nodes + static_cast<int64_t>(todo) * 4;
-      const float4 a = n[0], b = n[1], c = n[2];
-      const int4 ch = *reinterpret_cast<const int4*>(n + 3);
-      if (COUNT) cnt.box += 2;
-      // left box lo=(a.x,a.y,a.z) hi=(a.w,b.x,b.y); right lo=(b.z,b.w,c.x) hi=(c.y,c.z,c.w)
-      const float l0x = fmaf(a.x, inv.x, oi.x), l1x = fmaf(a.w, inv.x, oi.x);
-      const float l0y = fmaf(a.y, inv.y, oi.y), l1y = fmaf(b.x, inv.y, oi.y);
-      const float l0z = fmaf(a.z, inv.z, oi.z), l1z = fmaf(b.y, inv.z, oi.z);
-      const float r0x = fmaf(b.z, inv.x, oi.x), r1x = fmaf(c.y, inv.x, oi.x);
-      const float r0y = fmaf(b.w, inv.y, oi.y), r1y = fmaf(c.z, inv.y, oi.y);
-      const float r0z = fmaf(c.x, inv.z, oi.z), r1z = fmaf(c.w, inv.z, oi.z);
-      const float ln = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), kTMin));
-      const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tbest));
-      const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kTMin));
-      const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tbest));
-      // An empty slot (right child only; the host guarantees the left one is never empty) has an
-      // inverted box, which the symmetric min/max slab form would report as all of space: test
-      // the child code explicitly.
-      const bool hl = ln <= lf;
-      const bool hr = rn <= rf && ch.y != kEmptyChild;
-      if (hl && hr) {
-        const bool lfirst = ln <= rn;
-        const int32_t nearc = lfirst ? ch.x : ch.y;
-        const int32_t farc = lfirst ? ch.y : ch.x;
-        if (sp < STACK) {
-          stk[sp * 64] = farc;
-          ++sp;
-        } else {
-          overflow = true;
-        }
-        todo = nearc;
-        continue;
-      }
-      if (hl || hr) {
-        todo = hl ? ch.x : ch.y;
-        continue;
-      }
-    } else {
-      const int32_t code = ~todo;
-      const int32_t first = code >> 3;
-      const int32_t count = (code & 7) + 1;
-      if (static_cast<int64_t>(first) + count > S.num_refs) {
-        corrupt = true;
-        break;
-      }
-      for (int k = 0; k < count; ++k) {
-        const int32_t ref = S.refs[first + k];
-        float t;
-        if (COUNT) cnt.prim += 1;
-        bool take;
-        if (ref & kQuadRefBit) {
-          int32_t qrank = -1;
-          t = ref == origin ? -1.0f
-                            : quad_t(S.quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5, o, d, kTMin, tbest, -2,
-                                     qrank);
-          take = t > 0.0f && (t < tbest || quad_wins_tie(S, qrank, best));
-        } else {
-          const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
-          t = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
-          take = t > 0.0f;
-        }
-        if (take) {  // t > tmin >= 0.001
-          tbest = t;
-          best = ref;
-        }
-      }
-    }
-    if (sp == 0) break;
-    --sp;
-    todo = stk[sp * 64];
-  }
-  return best;
-}
-
 // ---------------------------------------------------------------------------------------
 // Textures (texture.hpp:34-151, perlin.hpp:95-158, 219-255)
 __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
@@ -1059,27 +952,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
-// Lane -> pixel mapping: a wave covers an 8x8 tile of the shard (rows are shard-local).
-struct LanePixel {
-  int i, lr, j;
-  uint32_t pixel_id;
-  bool valid;
-};
-__device__ __forceinline__ LanePixel tile_pixel(const DevCamera& C, const DevJob& J, int tx, int ty,
-                                                int lane) {
-  LanePixel p;
-  p.i = tx * 8 + (lane & 7);
-  p.lr = ty * 8 + (lane >> 3);
-  p.valid = p.i < C.width && p.lr < J.row_count;
-  p.j = J.row_begin + p.lr * J.row_stride;
-  p.pixel_id = static_cast<uint32_t>(p.j) * static_cast<uint32_t>(C.width) + static_cast<uint32_t>(p.i);
-  return p;
-}
-// non-persistent grids: a 256-thread workgroup covers 16x16 pixels (2x2 wave tiles)
-__device__ __forceinline__ LanePixel lane_pixel(const DevCamera& C, const DevJob& J, int lane, int wave) {
-  return tile_pixel(C, J, blockIdx.x * 2 + (wave & 1), blockIdx.y * 2 + (wave >> 1), lane);
-}
-
 // Per-wave accumulators that outlive one tile.
 template <bool COUNT>
 struct WaveStats {
@@ -1119,15 +991,6 @@ __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w
   if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
   if (__any(w.overflow) && lane == 0) atomicAdd(&J.counters[4], 1ull);
   if (__any(w.corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
-}
-
-__device__ __forceinline__ void store_pixel(const DevCamera& C, const DevJob& J, const LanePixel& px, V3 acc) {
-  if (px.valid) {
-    float* o = J.out + (static_cast<int64_t>(px.lr) * C.width + px.i) * 3;
-    o[0] = C.scale * acc.x;
-    o[1] = C.scale * acc.y;
-    o[2] = C.scale * acc.z;
-  }
 }
 
 // A lane's pixel, packed: column in the low 16 bits, shard-local row in the high 16 bits.
@@ -1743,119 +1606,6 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
 
 
 
-// Schedule 1: each loop trip runs one complete closest-hit query per lane through trav_step, so
-// the wave waits for its slowest traversal every segment.
-template <int STACK, bool COUNT>
-__global__ __launch_bounds__(256) void render_kernel_segment(DevScene S, DevCamera C, DevJob J) {
-  __shared__ int32_t s_stack[4 * STACK * 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  int32_t* stk = s_stack + wave * STACK * 64 + lane;
-  const LanePixel px = lane_pixel(C, J, lane, wave);
-
-  V3 acc = v3(0.0f, 0.0f, 0.0f);
-  uint32_t segs = 0, hits = 0;
-  Counts<COUNT> cnt;
-  bool overflow = false, corrupt = false;
-  int sample = (px.valid && C.max_depth > 0) ? 0 : C.spp;
-  PathState ps;
-  if (sample < C.spp) start_sample(ps, C, J.seed_mix, px.pixel_id, 0, px.i, px.j);
-  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
-  while (sample < C.spp) {
-    Trav tr;
-    trav_begin(tr, S, ps.o, ps.d, ps.origin);
-    while (trav_active(tr))
-      trav_step<LdsStack<STACK>, COUNT>(tr, S, ps.o, ps.d, ps.time, LdsStack<STACK>{stk}, cnt, overflow, corrupt);
-    ++segs;
-    bool alive;
-    if (tr.best < 0) {
-      ps.L = vfma(ps.T, bg, ps.L);
-      alive = false;
-    } else {
-      if (COUNT) ++hits;
-      alive = shade<true>(S, ps, tr.best, tr.tbest);
-      if (alive && --ps.depth <= 0) alive = false;
-    }
-    if (!alive) {
-      acc = add(acc, ps.L);
-      ++sample;
-      if (sample < C.spp) start_sample(ps, C, J.seed_mix, px.pixel_id, sample, px.i, px.j);
-    }
-  }
-  store_pixel(C, J, px, acc);
-  WaveStats<COUNT> w;
-  w.segs = segs;
-  w.hits = hits;
-  w.cnt = cnt;
-  w.overflow = overflow;
-  w.corrupt = corrupt;
-  flush_stats<COUNT>(J, w, lane);
-}
-
-// Schedule 2: the first kernel (monolithic closest_hit loop), kept for A/B.
-template <int STACK, bool COUNT>
-__global__ __launch_bounds__(256) void render_kernel_v0(DevScene S, DevCamera C, DevJob J) {
-  __shared__ int32_t s_stack[4 * STACK * 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  int32_t* stk = s_stack + wave * STACK * 64 + lane;
-  const int i = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-  const bool valid = i < C.width && lr < J.row_count;
-  const int j = J.row_begin + lr * J.row_stride;
-  const uint32_t pixel_id = static_cast<uint32_t>(j) * static_cast<uint32_t>(C.width) +
-                            static_cast<uint32_t>(i);
-
-  V3 acc = v3(0.0f, 0.0f, 0.0f);
-  uint32_t segs = 0, hits = 0;
-  Counts<COUNT> cnt;
-  bool overflow = false, corrupt = false;
-  int sample = (valid && C.max_depth > 0) ? 0 : C.spp;
-  PathState ps;
-  if (sample < C.spp) start_sample(ps, C, J.seed_mix, pixel_id, 0, i, j);
-  const V3 bg = v3(C.background[0], C.background[1], C.background[2]);
-  while (sample < C.spp) {
-    float t = __builtin_inff();
-    const int32_t ref =
-        closest_hit<STACK, COUNT>(S, ps.o, ps.d, ps.time, ps.origin, t, stk, cnt, overflow, corrupt);
-    ++segs;
-    bool alive;
-    if (ref < 0) {
-      ps.L = vfma(ps.T, bg, ps.L);
-      alive = false;
-    } else {
-      if (COUNT) ++hits;
-      alive = shade<true>(S, ps, ref, t);
-      if (alive && --ps.depth <= 0) alive = false;
-    }
-    if (!alive) {
-      acc = add(acc, ps.L);
-      ++sample;
-      if (sample < C.spp) start_sample(ps, C, J.seed_mix, pixel_id, sample, i, j);
-    }
-  }
-  if (valid) {
-    float* o = J.out + (static_cast<int64_t>(lr) * C.width + i) * 3;
-    o[0] = C.scale * acc.x;
-    o[1] = C.scale * acc.y;
-    o[2] = C.scale * acc.z;
-  }
-  const uint32_t wsegs = wave_sum(segs);
-  if (COUNT) {
-    const uint32_t wbox = wave_sum(cnt.box);
-    const uint32_t wprim = wave_sum(cnt.prim);
-    const uint32_t whits = wave_sum(hits);
-    if (lane == 0) {
-      atomicAdd(&J.counters[1], static_cast<unsigned long long>(wbox));
-      atomicAdd(&J.counters[2], static_cast<unsigned long long>(wprim));
-      atomicAdd(&J.counters[3], static_cast<unsigned long long>(whits));
-    }
-  }
-  if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
-  if (__any(overflow) && lane == 0) atomicAdd(&J.counters[4], 1ull);
-  if (__any(corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
-}
-
 // write_color (color.hpp:14-58) in the reference's own precision: linear_to_gamma takes the
 // square root in double (color.hpp:14-23), interval::clamp clamps in double to
 // [0.000f, 0.999f] (the float literals widened, color.hpp:45, interval.hpp:35-46), and
@@ -1921,20 +1671,6 @@ KernelChoice plain_kernel(bool count, bool ring) {
          : ring ? reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, false, WIDE, TEXF, true>)
                 : reinterpret_cast<const void*>(&render_kernel<STACK, SPILL, false, WIDE, TEXF, false>);
   k.block = 256;
-  return k;
-}
-
-template <int STACK>
-KernelChoice legacy_kernel(bool count, int variant) {
-  KernelChoice k;
-  if (variant == 2)
-    k.fn = count ? reinterpret_cast<const void*>(&render_kernel_v0<STACK, true>)
-                 : reinterpret_cast<const void*>(&render_kernel_v0<STACK, false>);
-  else
-    k.fn = count ? reinterpret_cast<const void*>(&render_kernel_segment<STACK, true>)
-                 : reinterpret_cast<const void*>(&render_kernel_segment<STACK, false>);
-  k.block = 256;
-  k.grid2d = true;
   return k;
 }
 
@@ -2009,18 +1745,7 @@ KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool c
   if (variant == 3 || variant == 0)
     return S.node_width == 4 ? default_kernel<4>(S, J, count, stack, variant == 3)
                              : default_kernel<2>(S, J, count, stack, variant == 3);
-  // schedules 1 and 2 traverse binary nodes only, without a scene-spanning occluder
-  if (S.node_width != 2 || S.occluder >= 0) return {};
-  switch (stack) {
-    case 16:
-      return legacy_kernel<16>(count, variant);
-    case 32:
-      return legacy_kernel<32>(count, variant);
-    case 64:
-      return legacy_kernel<64>(count, variant);
-    default:
-      return {};
-  }
+  return {};
 }
 
 hipError_t launch_render(const KernelChoice& k, const DevScene& S, const DevCamera& C, const DevJob& J,
@@ -2031,7 +1756,7 @@ hipError_t launch_render(const KernelChoice& k, const DevScene& S, const DevCame
     const hipError_t e = hipFuncSetAttribute(k.fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
     if (e != hipSuccess) return e;
   }
-  const dim3 grid = k.grid2d ? dim3((C.width + 15) / 16, (J.row_count + 15) / 16) : dim3(grid_blocks);
+  const dim3 grid(grid_blocks);
   DevScene s = S;
   DevCamera c = C;
   DevJob j = J;
@@ -2051,13 +1776,6 @@ KernelResources kernel_resources(const void* fn) {
   return r;
 }
 
-
-int kernel_stack_depth(int bvh_depth) {
-  if (bvh_depth <= 16) return 16;
-  if (bvh_depth <= 32) return 32;
-  if (bvh_depth <= 64) return 64;
-  return -1;
-}
 
 // Dynamic LDS bytes of the persistent kernel for this scene, or -1 when it does not fit in
 // one CU's 160 KiB; fills the scene-copy offsets of the job.

@@ -22,6 +22,7 @@ LIB_DIR = os.path.join(PKG_DIR, "lib")
 
 RTG_ABI_VERSION = 5
 RTG_OK = 0
+RTG_E_INVALID, RTG_E_HIP, RTG_E_NODEVICE, RTG_E_NOMEM, RTG_E_UNSUPPORTED = -1, -2, -3, -4, -5
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
 RTG_MAT_LAMBERTIAN, RTG_MAT_METAL, RTG_MAT_DIELECTRIC, RTG_MAT_DIFFUSE_LIGHT = 1, 2, 3, 4
 RTG_TEX_SOLID, RTG_TEX_CHECKER, RTG_TEX_IMAGE, RTG_TEX_NOISE = 1, 2, 3, 4

@@ -139,15 +139,14 @@ def test_bvh_mode_does_not_change_the_image(gpu_lib, scenes):
 
 
 def test_schedules_give_identical_frames(gpu_lib, scenes):
-    """All kernel schedules (persistent LDS-resident default, plain-grid ballot-batched,
-    per-segment, the first kernel) differ only in when a lane's work runs, never in what it
-    computes: identical frames and segment counts."""
+    """All kernel schedules (persistent LDS-resident default, plain-grid ballot-batched, the
+    treelet) differ only in when a lane's work runs, never in what it computes: identical frames
+    and segment counts. The retired per-segment schedules 1 and 2 report RTG_E_UNSUPPORTED."""
     import ctypes as C
 
     frames, segs = [], []
     for mode, flag_set in (
-            (rtgpu.RTG_BVH_MEDIAN, (0, rtgpu.RTG_RENDER_SCHEDULE(1), rtgpu.RTG_RENDER_SCHEDULE(2),
-                                    rtgpu.RTG_RENDER_SCHEDULE(3), rtgpu.RTG_RENDER_SCHEDULE(4))),
+            (rtgpu.RTG_BVH_MEDIAN, (0, rtgpu.RTG_RENDER_SCHEDULE(3), rtgpu.RTG_RENDER_SCHEDULE(4))),
             (2, (0, rtgpu.RTG_RENDER_SCHEDULE(4))),  # binary SAH
             (rtgpu.RTG_BVH_SAH, (0, rtgpu.RTG_RENDER_SCHEDULE(4), rtgpu.RTG_RENDER_LEAF_BATCH(1),
                                  rtgpu.RTG_RENDER_LEAF_BATCH(64), rtgpu.RTG_RENDER_SHADE_BATCH(1),
@@ -167,10 +166,19 @@ def test_schedules_give_identical_frames(gpu_lib, scenes):
             frames.append(out)
             segs.append(st.segments)
         ds.close()
-    # across BVH layouts only exact-t ties may resolve differently (H9)
-    assert all(np.mean(np.all(f == frames[0], axis=-1)) > 0.999 for f in frames)
-    assert all(np.array_equal(f, frames[0]) for f in frames[:5])  # same tree: bit-identical
-    assert max(segs) - min(segs) <= 2
+    # every tree and schedule: bit-identical (the spec's tie rule makes the closest hit order-free)
+    assert all(np.array_equal(f, frames[0]) for f in frames)
+    assert max(segs) == min(segs)
+    s = scenes.build("bouncing_spheres", rand_seed=1, bvh_mode=rtgpu.RTG_BVH_MEDIAN)
+    ds = gpu_lib.scene_create(s.desc)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 32, 1, 5
+    out = np.zeros((gpu_lib.camera_resolve(c).image_height, 32, 3), dtype=np.float32)
+    for sched in (1, 2):
+        job = rtgpu.rtg_render_desc(5, 0, 1, 0, rtgpu.RTG_RENDER_SCHEDULE(sched), None)
+        assert gpu_lib.lib.rtg_render(ds.handle, C.byref(c), C.byref(job), out.ctypes.data, None) == \
+            rtgpu.RTG_E_UNSUPPORTED
+    ds.close()
 
 
 @pytest.mark.parametrize("name,W,spp,depth", [("cornell_box", 96, 16, 100), ("earth_perlin", 128, 8, 50)])

@@ -251,30 +251,9 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   const float beta = dot(w, cross(u, hp));
   if (!(0.0f <= alpha && alpha <= 1.0f) || !(0.0f <= beta && beta <= 1.0f)) return -1.0f;
   rank = ibits(q2.w);
-#ifndef RTG_AB_NO_TIE
   if (t == tmax && rank <= brank) return -1.0f;
-#endif
   return t;
 }
-
-#ifdef RTG_AB_TIE_RELOAD
-// A/B: the LDS schedule's tie check without the closest hit's rank in the traversal state: on a root
-// equal to tmax (a branch the wave skips when no lane ties) the closest hit's rank is re-read from its
-// quad record (`quads`: the LDS copy), so Trav::mat is not live across the traversal loop
-__device__ __forceinline__ float quad_t_reload(const float4* q, V3 o, V3 d, float tmin, float tmax,
-                                               const float4* quads, int32_t best) {
-  int32_t rank = -1;
-  const float t = quad_t(q, o, d, tmin, tmax, -2, rank);
-#ifndef RTG_AB_NO_TIE
-  if (t == tmax) {
-    const int32_t brank = (best >= 0 && (best & kQuadRefBit))
-                              ? ibits(quads[static_cast<int64_t>(best & ~kQuadRefBit) * 5 + 2].w) : -1;
-    if (rank <= brank) return -1.0f;
-  }
-#endif
-  return t;
-}
-#endif
 
 // Exact-t ties (rtg-f32 spec, DESIGN.md §4 "tie rule"). The reference tests the world's objects in
 // list order (hittable_list.hpp:40-64) against a shrinking interval: quad::hit accepts t ==
@@ -287,9 +266,7 @@ __device__ __forceinline__ float quad_t_reload(const float4* q, V3 o, V3 d, floa
 // check is one compare and a wave-uniform branch). Two spheres at the bit-identical t (duplicate
 // spheres, a ray through a tangent point) keep the one tested first: the one order-dependent case,
 // left out of the rule because its compare cost config 2 3 %.
-#ifndef RTG_AB_NO_TIE
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-#endif
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
@@ -649,19 +626,12 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       // is a sphere or an earlier quad of the list. LDS schedule: t.mat holds the closest hit's rank and
       // quad_t rejects a losing tie on its hit path; cache-read schedules (t.mat = material): the rank
       // is re-read, only on a tie
-#ifdef RTG_AB_TIE_RELOAD
-      if constexpr (!MAT)
-        th = ref == t.origin ? -1.0f : quad_t_reload(q, o, d, kTMin, t.tbest, S.quads, t.best);
-      else
-#endif
-        th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, MAT ? -2 : t.mat, qrank);
+      th = ref == t.origin ? -1.0f : quad_t(q, o, d, kTMin, t.tbest, MAT ? -2 : t.mat, qrank);
       if (MAT && th > 0.0f) m = ibits(q[1].w);
       take = th > 0.0f;
-#ifndef RTG_AB_NO_TIE
       if constexpr (MAT) {
         if (ballot_tie(th == t.tbest) != 0 && th == t.tbest) take = quad_wins_tie(S, qrank, t.best);
       }
-#endif
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
@@ -692,25 +662,6 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
   const int py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
   const int pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
   float accum = 0.0f;
-#ifdef RTG_AB_PERLIN8  // A/B only: round 2's eight float4 gradients fetched at once
-  float4 g[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) g[c] = vec[px[c >> 2] ^ py[(c >> 1) & 1] ^ pz[c & 1]];
-#pragma unroll
-  for (int di = 0; di < 2; ++di)
-#pragma unroll
-    for (int dj = 0; dj < 2; ++dj)
-#pragma unroll
-      for (int dk = 0; dk < 2; ++dk) {
-        const V3 c = xyz(g[di * 4 + dj * 2 + dk]);
-        const V3 wv = v3(u - di, v - dj, w - dk);
-        const float fu = di ? uu : (1.0f - uu);
-        const float fv = dj ? vv : (1.0f - vv);
-        const float fw = dk ? ww : (1.0f - ww);
-        accum = fmaf(fu * fv * fw, dot(c, wv), accum);
-      }
-  return accum;
-#endif
   // the corner gradients in pairs (di, dj fixed; dk = 0, 1), each pair fetched (xyz only) before it
   // is used and the sum in the reference's corner order: fetching all eight float4s at once (round 2)
   // saved LDS round trips but made the textured kernel spill its path state to scratch at 5 waves
@@ -1039,11 +990,7 @@ __device__ __forceinline__ bool ring_slot_free(const DevJob& J, int tile) {
 // A unit's partial sum: 16 B per lane, one write-through store (aux 16 = sc1).
 __device__ __forceinline__ void ring_store(__amdgpu_buffer_rsrc_t rs, uint32_t unit, V3 a) {
   const ring_u4 v = {__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), 0u};
-#if defined(RTG_AB_RING_PLAINSTORE) || defined(RTG_RING_RELEASE)
-  __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>(unit << 4), 0, 0);
-#else
   __builtin_amdgcn_raw_buffer_store_b128(v, rs, static_cast<int>(unit << 4), 0, 16);
-#endif
 }
 
 // The tile's combine, by the wave whose ticket add was the tile's last: ONE agent acquire, the
@@ -1113,13 +1060,7 @@ __device__ __forceinline__ void ring_combine(__amdgpu_buffer_rsrc_t rs, const De
 template <bool WIDE_REGS>
 __device__ __forceinline__ void ring_batch_done(__amdgpu_buffer_rsrc_t rs, const DevCamera& C, const DevJob& J,
                                                 int tile) {
-#ifdef RTG_RING_RELEASE  // plain partial stores: drain, agent release (L2 write-back), drain again
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#elif !defined(RTG_AB_RING_NOWAIT)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have landed
-#endif
   const int R = 1 << J.ring_log2;
   const int slot = tile & (R - 1);
   const uint32_t gen = static_cast<uint32_t>(tile >> J.ring_log2);
@@ -1128,11 +1069,6 @@ __device__ __forceinline__ void ring_batch_done(__amdgpu_buffer_rsrc_t rs, const
     old = __hip_atomic_fetch_add((gu32*)(J.ring_words + R + slot), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   old = __builtin_amdgcn_readfirstlane(old);
   if (old + 1u != (gen + 1u) * static_cast<uint32_t>(J.chunks)) return;
-#ifdef RTG_AB_RING_NOCOMBINE
-  if (__lane_id() == 0)
-    __hip_atomic_store((gu32*)(J.ring_words + slot), gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return;
-#endif
   ring_combine<WIDE_REGS>(rs, C, J, tile, slot);
 }
 
@@ -1402,11 +1338,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         } else {
           const int64_t pix = static_cast<int64_t>(px_lr(px)) * C.width + px_i(px);
           if (ring) {  // the unit's partial sum into its tile's ring slot (settled next trip)
-#ifdef RTG_AB_RING_NOSTORE
-            asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(chunk));  // probe: keep the values, skip the store
-#else
             ring_store(ring_rs, static_cast<uint32_t>(chunk & 0x0fffffff), acc);
-#endif
             fin = true;
           } else if (J.partial == nullptr) {  // one chunk per pixel: the pixel mean directly
             float* o = J.out + pix * 3;
@@ -1415,15 +1347,9 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
             o[2] = C.scale * acc.z;
           } else {  // progressive: chunk partial sum in the full-frame layout, combined by combine_kernel
             float* o = J.partial + (static_cast<int64_t>(chunk) * J.row_count * C.width + pix) * 3;
-#ifdef RTG_AB_BASE_SC1  // probe: the full-frame partials stored write-through
-            __hip_atomic_store((gu32*)o, __float_as_uint(acc.x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((gu32*)(o + 1), __float_as_uint(acc.y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store((gu32*)(o + 2), __float_as_uint(acc.z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
             o[0] = acc.x;
             o[1] = acc.y;
             o[2] = acc.z;
-#endif
           }
           s_end = 0;  // the unit is done
           ++w.pixels;
@@ -1680,11 +1606,7 @@ KernelChoice treelet_kernel(const DevScene& S, const DevJob& J, bool count) {
   const bool spill = J.spill_depth > 0, tex = S.tex_full != 0, ring = J.ring_log2 >= 0 && !count;
   if (S.node_width != 4) return {};
   // sphere-only scenes (the 1M field) get a build without the quad test (kPrimsSpheres, as default_kernel)
-#ifndef RTG_AB_PRIMS_ANY
   const bool spheres = S.ref_mode == 1 && !tex;
-#else
-  const bool spheres = false;
-#endif
   if (spill)
     return tex ? lds_kernel<kLdsStack, true, 4, true, kGeomTreelet>(count, ring)
                : spheres ? lds_kernel<kLdsStack, true, 4, false, kGeomTreelet, kLdsWaves, kPrimsSpheres>(count, ring)
@@ -1712,17 +1634,9 @@ KernelChoice default_kernel(const DevScene& S, const DevJob& J, bool count, int 
       return tex ? lds_kernel<kLdsStack, true, WIDE, true>(count, ring) : lds_kernel<kLdsStack, true, WIDE, false>(count, ring);
     // 4-wide trees with 16-bit stacks: the 4-wave build for both workgroup shapes (see render_kernel_lds),
     // one per primitive class (kPrimsAny...: the leaf test compiled for the scene's primitives only)
-#ifndef RTG_AB_PRIMS_ANY
     // (a quad-only tree with a sphere occluder beside it shades spheres too: kPrimsAny)
     const int kind = S.ref_mode == 1 ? kPrimsSpheres : (S.ref_mode == 2 && S.occluder < 0 ? kPrimsQuads : kPrimsAny);
-#ifndef RTG_AB_NO_DIFFUSE_CLASS
     const int prims = kind | (S.diffuse_only ? kPrimsDiffuse : 0);
-#else
-    const int prims = kind;
-#endif
-#else
-    const int prims = kPrimsAny;  // A/B: one leaf test for every scene (round 4)
-#endif
     if (WIDE == 4 && !tex && J.lds_waves == kLdsWaves)
       return lds4_kernel<false>(prims, count, ring, kLdsWaves * 64);
     if (WIDE == 4 && J.lds_waves == 4)  // small scenes: five 4-wave workgroups per CU; the dual's second launch

@@ -902,10 +902,11 @@ static float sphere_t32(const float* s, f3 o, f3 d, float time, float tmin, floa
   if (fabsf(q) < 0x1p-100f || a == 0.0f) return -1.0f;
   float t0 = q * inv_a, t1 = c / q; /* far root by the reciprocal, near root divided */
   float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
-  /* roots strictly inside (tmin, tmax) (interval::surrounds): a sphere never replaces an equal-t hit */
-  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
-  if (tmin < lo && lo < tmax) return lo;
-  if (tmin < hi && hi < tmax) return hi;
+  /* roots in (tmin, tmax]: strictly above tmin (interval::surrounds, sphere.hpp:70); a root equal to
+     tmax is returned for the exact-t tie rule (sphere_wins_tie32) to decide, round 5 */
+  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
+  if (tmin < lo && lo <= tmax) return lo;
+  if (tmin < hi && hi <= tmax) return hi;
   return -1.0f;
 }
 /* quad::hit, fp32: returns t or -1 */
@@ -925,14 +926,18 @@ static float quad_t32(const float* q, f3 o, f3 d, float tmin, float tmax) {
   return t;
 }
 
-/* Exact-t tie rule of the rtg-f32 spec (rtg_kernels.hip quad_wins_tie): the reference tests
-   its list in order (hittable_list.hpp:40-64), quads accept t == closest (interval::contains,
-   quad.hpp:62), spheres do not (interval::surrounds, sphere.hpp:70). At equal t a quad replaces a sphere
-   and an earlier quad of the list, whatever order they are tested in; a sphere replaces nothing
-   (sphere_t32's strict bound). ids are input (list-order) indices. */
+/* Exact-t tie rule of the rtg-f32 spec (rtg_kernels.hip quad_wins_tie / sphere_wins_tie):
+   the reference tests its list in order (hittable_list.hpp:40-64), quads accept t == closest
+   (interval::contains, quad.hpp:62), spheres do not (interval::surrounds, sphere.hpp:70). So among the
+   primitives at the smallest t the last quad of the list wins if there is one, else the first sphere,
+   whatever order they are tested in: at equal t a quad replaces a sphere and an earlier quad, a sphere
+   replaces a later sphere (round 5) and no quad. ids are input (list-order) indices. */
 static int quad_wins_tie32(const world32* w, int64_t id, int64_t best) {
   if (w->s->prims[best].kind != RTG_PRIM_QUAD) return 1;
   return id > best;
+}
+static int sphere_wins_tie32(const world32* w, int64_t id, int64_t best) {
+  return best >= 0 && w->s->prims[best].kind == RTG_PRIM_SPHERE && id < best;
 }
 
 /* closest hit: reference BVH order; boxes tested in f64 (pure culling), primitives in fp32 */
@@ -946,7 +951,8 @@ static void node_hit32(const world32* w, int32_t code, f3 o, f3 d, const double 
                   ? sphere_t32(w->sph + id * 8, o, d, time, 0.001f, *tbest, id == origin)
                   : (id == origin ? -1.0f : quad_t32(w->qd + id * 16, o, d, 0.001f, *tbest));
     int take = t > 0.0f;
-    if (take && w->s->prims[id].kind == RTG_PRIM_QUAD && t == *tbest) take = quad_wins_tie32(w, id, *best);
+    if (take && t == *tbest)
+      take = w->s->prims[id].kind == RTG_PRIM_QUAD ? quad_wins_tie32(w, id, *best) : sphere_wins_tie32(w, id, *best);
     if (take) {
       *tbest = t;
       *best = id;
@@ -1233,10 +1239,12 @@ int orc_kat_sphere_hit(const rtg_primitive* p, const double o[3], const double d
   }
   return h;
 }
-/* the rtg-f32 sphere test (sphere_t32) on one record {center, r, motion, material}: t or -1 */
+/* the rtg-f32 sphere test (sphere_t32) on one record {center, r, motion, material}: t or -1, a root
+   inside (tmin, tmax) as sphere::hit accepts it (a root equal to tmax, which the tie rule sees, is a miss) */
 float orc_sphere_t32(const float s[8], const float o[3], const float d[3], float time, float tmin,
                      float tmax) {
-  return sphere_t32(s, F3(o[0], o[1], o[2]), F3(d[0], d[1], d[2]), time, tmin, tmax, 0);
+  const float t = sphere_t32(s, F3(o[0], o[1], o[2]), F3(d[0], d[1], d[2]), time, tmin, tmax, 0);
+  return t == tmax ? -1.0f : t;
 }
 int orc_kat_quad_hit(const rtg_primitive* p, const double o[3], const double d[3], double tmin,
                      double tmax, double rec[10], double bbox[6]) {

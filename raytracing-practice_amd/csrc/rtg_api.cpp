@@ -22,6 +22,7 @@
 namespace rtg {
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,
                           hipStream_t stream);
+hipError_t launch_repad(float* nodes, int64_t num_nodes, int width, float delta, hipStream_t stream);
 KernelChoice choose_kernel(const DevScene& S, const DevJob& J, int stack, bool count, int variant);
 hipError_t launch_render(const KernelChoice& k, const DevScene& S, const DevCamera& C, const DevJob& J,
                          int lds_bytes, int grid_blocks, hipStream_t stream);
@@ -123,6 +124,19 @@ float round_up(double x) {
   if (static_cast<double>(f) < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
   return f;
 }
+// Culling margin (DESIGN.md §4 "conservative culling"): every BVH box plane the kernels test is moved
+// outward by eta = 2^-21 (|plane| + M) before its fp32 rounding (itself outward), where M bounds
+// |coordinate| of every ray origin (primitive boxes, the camera). The kernels' slab test
+// fma(plane, rcp(d), -o rcp(d)) errs by at most 3 2^-24 |plane - o| + 2^-24 |o| in world units along
+// the axis (v_rcp_f32: 1 ulp), i.e. < eta / 2: a computed entry (exit) distance is then never past the
+// unpadded box's true one, so no box holding a primitive hit is culled by rounding.
+float pad_down(double lo, double m) {
+  return std::isfinite(lo) ? round_down(lo - 0x1p-21 * (std::fabs(lo) + m)) : static_cast<float>(lo);
+}
+float pad_up(double hi, double m) {
+  return std::isfinite(hi) ? round_up(hi + 0x1p-21 * (std::fabs(hi) + m)) : static_cast<float>(hi);
+}
+
 float ibits_to_float(int32_t i) {
   float f;
   std::memcpy(&f, &i, 4);
@@ -276,6 +290,7 @@ void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
 // kEmptyChild with the inverted box (+inf, -inf). Boxes rounded outward to fp32.
 template <int W>
 bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
+  const double M = out->origin_bound;
   constexpr int64_t kBytes = node_bytes(W), kWords = 7 * W;
   if (t.nodes.size() > static_cast<size_t>(INT32_MAX / kBytes)) {
     *err = "BVH too large for 32-bit node offsets";
@@ -308,8 +323,8 @@ bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
           }
         }
         for (int a = 0; a < 3; ++a) {
-          f[a * W + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
-          f[3 * W + a * W + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
+          f[a * W + c] = empty ? std::numeric_limits<float>::infinity() : pad_down(n.lo[c][a], M);
+          f[3 * W + a * W + c] = empty ? -std::numeric_limits<float>::infinity() : pad_up(n.hi[c][a], M);
         }
         f[6 * W + c] = ibits_to_float(code);
       }
@@ -365,6 +380,28 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     }
     if (p.material < 0 || p.material >= d->num_materials) {
       *err = "primitive material index out of range at index " + std::to_string(i);
+      return false;
+    }
+  }
+  // M of the culling margin (pad_down): the largest |coordinate| of any primitive box, i.e. of any hit
+  // point a later segment starts from; rtg_render widens the pad when a camera lies farther out
+  {
+    const int T = host_threads(d->num_prims);
+    std::vector<double> part(T, 0.0);
+    host_par_for(d->num_prims, [&](int64_t b, int64_t e, int t) {
+      double m = 0.0;
+      for (int64_t i = b; i < e; ++i) {
+        double lo[3], hi[3];
+        prim_bbox(d->prims[i], lo, hi);
+        for (int a = 0; a < 3; ++a) m = std::max({m, std::fabs(lo[a]), std::fabs(hi[a])});
+        if (!std::isfinite(lo[0] + lo[1] + lo[2] + hi[0] + hi[1] + hi[2])) m = HUGE_VAL;
+      }
+      part[t] = m;
+    });
+    out->origin_bound = 0.0;
+    for (const double m : part) out->origin_bound = std::max(out->origin_bound, m);
+    if (!(out->origin_bound < 1e30)) {
+      *err = "primitive coordinates are not finite (or above 1e30)";
       return false;
     }
   }
@@ -561,8 +598,8 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         continue;
       }
       for (int a = 0; a < 3; ++a) {
-        lo[s][a] = round_down(n.lo[s][a]);
-        hi[s][a] = round_up(n.hi[s][a]);
+        lo[s][a] = pad_down(n.lo[s][a], out->origin_bound);
+        hi[s][a] = pad_up(n.hi[s][a], out->origin_bound);
       }
       if (n.child[s] >= 0) {
         code[s] = n.child[s];
@@ -731,6 +768,9 @@ struct rtg_scene {
   // host copy of the device node array in its current order (scenes on the treelet schedule): the hot
   // treelet renumbers this copy and uploads it, so a tuning downloads only the visit counts
   std::vector<int32_t> host_nodes;
+  // M of the culling margin the device node boxes are padded for (HostScene::origin_bound); raised,
+  // with the boxes, when a camera lies farther out (ensure_origin_bound)
+  double origin_bound = 0.0;
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
@@ -910,7 +950,8 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     GpuBvhResult r{};
     e = gpu_build_bvh4(reinterpret_cast<const float4*>(base + parts[2].off),
                        reinterpret_cast<const float4*>(base + parts[3].off), refs_dev, nrefs,
-                       reinterpret_cast<float*>(base + parts[0].off), hs.node_capacity, sorted, &r, s->own_stream);
+                       round_up(0x1p-21 * hs.origin_bound), reinterpret_cast<float*>(base + parts[0].off),
+                       hs.node_capacity, sorted, &r, s->own_stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(refs_dev, sorted, nrefs * 4, hipMemcpyDeviceToDevice, s->own_stream);
     const hipError_t ef = hipFreeAsync(sorted, s->own_stream);
@@ -978,6 +1019,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     s->host_nodes.assign(reinterpret_cast<const int32_t*>(hs.nodes.data()),
                          reinterpret_cast<const int32_t*>(hs.nodes.data()) + hs.nodes.size());
 
+  s->origin_bound = hs.origin_bound;
   s->info.device = device;
   s->info.bvh_mode = desc->bvh_mode;
   s->info.num_prims = hs.num_prims;
@@ -1441,6 +1483,30 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   return RTG_OK;
 }
 
+// The culling margin covers ray origins with |coordinate| <= s->origin_bound (the primitive boxes when the
+// scene was created). A camera whose lens reaches farther out widens the pad of every node box on the
+// device first (repad_nodes_kernel, on the render's stream; 1/16 headroom so a camera moving about does
+// not repad every frame). Boxes only grow: frames are unchanged, the conservative bound holds again.
+rtg_status ensure_origin_bound(rtg_scene* s, const rtg_camera_desc* cam, hipStream_t stream) {
+  if (s->dev.num_nodes <= 0) return RTG_OK;
+  rtg_camera_params cp;
+  resolve_camera(cam, &cp);
+  double mc = 0.0;
+  for (int a = 0; a < 3; ++a)
+    mc = std::max(mc, std::fabs(cp.center[a]) + std::fabs(cp.defocus_disk_u[a]) + std::fabs(cp.defocus_disk_v[a]));
+  if (mc <= s->origin_bound) return RTG_OK;
+  if (!(mc < 1e30)) return fail(RTG_E_INVALID, "camera position not finite (or above 1e30)");
+  const double target = mc * (1.0 + 1.0 / 16.0);
+  const float delta = round_up(0x1p-21 * (target - s->origin_bound));
+  RTG_HIP(launch_repad(reinterpret_cast<float*>(const_cast<float4*>(s->dev.nodes)), s->dev.num_nodes,
+                       s->dev.node_width, delta, stream),
+          "repad kernel launch");
+  s->origin_bound = target;
+  s->host_nodes.clear();  // the hot treelet downloads the repadded array when it next tunes
+  if (s->knobs.verbose) std::fprintf(stderr, "[rtg] culling margin widened for origins up to %.6g\n", target);
+  return RTG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1548,6 +1614,8 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
 
   RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
   hipStream_t stream = job->stream ? static_cast<hipStream_t>(job->stream) : s->own_stream;
+  pst = ensure_origin_bound(s, cam, stream);
+  if (pst != RTG_OK) return pst;
   const size_t out_bytes = P.out_bytes;
   float* dout = out_rgb;
   if (!P.dev_out && out_rgb) {  // a scene-owned device frame (not the stream-ordered pool)

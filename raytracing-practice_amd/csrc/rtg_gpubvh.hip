@@ -33,12 +33,15 @@ struct Box6 {
   float lo[3], hi[3];
 };
 
-__device__ __forceinline__ float pad_lo(float v) { return v - (fabsf(v) * 4.8e-7f + 1e-30f); }
-__device__ __forceinline__ float pad_hi(float v) { return v + (fabsf(v) * 4.8e-7f + 1e-30f); }
+// The culling margin of the host builder (rtg_api.cpp pad_down; DESIGN.md §4 "conservative culling"):
+// planes move outward by 2^-21 (|v| + M) for the slab test's rounding, here 2^-20 |v| + pad_abs
+// (pad_abs >= 2^-21 M, rounded up on the host) so that the box's own fp32 arithmetic (centre +- r, the
+// corner sums, this subtraction: a few 2^-24 |v|) is covered as well
+__device__ __forceinline__ float pad_lo(float v, float pad_abs) { return v - (fabsf(v) * 0x1p-20f + pad_abs); }
+__device__ __forceinline__ float pad_hi(float v, float pad_abs) { return v + (fabsf(v) * 0x1p-20f + pad_abs); }
 
-// Box of one primitive record (the fp32 records the render kernels intersect), padded outward
-// by a few ulps so the fp32 slab test only culls; thin axes get the reference's 0.0001 minimum
-// extent (aabb::pad_to_minimums, aabb.hpp:135-154).
+// Box of one primitive record (the fp32 records the render kernels intersect), unpadded; thin axes get
+// the reference's 0.0001 minimum extent (aabb::pad_to_minimums, aabb.hpp:135-154).
 __device__ Box6 prim_box(const float4* spheres, const float4* quads, int32_t ref) {
   Box6 b;
   if (ref & kQuadRefBit) {
@@ -69,8 +72,6 @@ __device__ Box6 prim_box(const float4* spheres, const float4* quads, int32_t ref
       b.lo[k] -= 0.00005f;
       b.hi[k] += 0.00005f;
     }
-    b.lo[k] = pad_lo(b.lo[k]);
-    b.hi[k] = pad_hi(b.hi[k]);
   }
   return b;
 }
@@ -85,14 +86,18 @@ __device__ __forceinline__ float o2f(uint32_t u) {
 }
 
 __global__ void prim_bounds_kernel(const float4* spheres, const float4* quads, const int32_t* refs, int64_t n,
-                                   Box6* boxes, uint32_t* cbounds) {
+                                   float pad_abs, Box6* boxes, uint32_t* cbounds) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   float c[3] = {0.0f, 0.0f, 0.0f};
   const bool ok = i < n;
   if (ok) {
-    const Box6 b = prim_box(spheres, quads, refs[i]);
+    Box6 b = prim_box(spheres, quads, refs[i]);
+    for (int k = 0; k < 3; ++k) {  // centroid of the unpadded box: Morton codes independent of the margin
+      c[k] = 0.5f * (b.lo[k] + b.hi[k]);
+      b.lo[k] = pad_lo(b.lo[k], pad_abs);
+      b.hi[k] = pad_hi(b.hi[k], pad_abs);
+    }
     boxes[i] = b;
-    for (int k = 0; k < 3; ++k) c[k] = 0.5f * (b.lo[k] + b.hi[k]);
   }
   for (int k = 0; k < 3; ++k) {
     uint32_t mn = ok ? f2o(c[k]) : 0xffffffffu, mx = ok ? f2o(c[k]) : 0u;
@@ -343,7 +348,7 @@ unsigned blocks_for(int64_t n) { return static_cast<unsigned>((n + 255) / 256); 
 // Builds the 4-wide BVH of n primitive refs (refs_in: input order) on the device. Writes up to
 // max_nodes nodes (28 floats each) to `nodes` and the leaf-ordered refs to `refs_out` (n entries).
 hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int32_t* refs_in, int64_t n,
-                          float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
+                          float pad_abs, float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
                           hipStream_t st) {
   *res = GpuBvhResult{};
   if (n <= 0) return hipSuccess;
@@ -395,7 +400,7 @@ hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int3
     const uint32_t cb_init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
     if ((err = hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, st)) != hipSuccess) break;
     hipLaunchKernelGGL(prim_bounds_kernel, dim3(blocks_for(n)), dim3(256), 0, st, spheres, quads, refs_in, n,
-                       boxes, cb);
+                       pad_abs, boxes, cb);
     hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(n)), dim3(256), 0, st, boxes, n, cb, codes, ids);
     if ((err = rocprim::radix_sort_pairs(P(o_sort), sort_bytes, codes, codes2, ids, ids2, static_cast<size_t>(n), 0,
                                          30, st)) != hipSuccess)

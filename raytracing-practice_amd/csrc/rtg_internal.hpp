@@ -48,6 +48,9 @@ struct HostScene {
   int64_t occluder_prim = -1;  // input primitive kept out of the BVH (a sphere; -1: none)
   int32_t occluder = -1;       // its sphere index (stored after the BVH-referenced spheres)
   int64_t node_capacity = 0;  // gpu_bvh: 4-wide nodes to reserve
+  // M of the culling margin: the node boxes are padded for ray origins with |coordinate| <= M
+  // (rtg_api.cpp pad_down; DESIGN.md §4 "conservative culling")
+  double origin_bound = 0.0;
   double bvh_ms = 0.0, collapse_ms = 0.0;  // host build phases (rtg_scene_info)
 };
 
@@ -203,8 +206,10 @@ struct GpuBvhResult {  // rtg_gpubvh.hip
   int32_t depth;
   int32_t stack_need;
 };
+// pad_abs: the culling margin's origin term (>= 2^-21 M, HostScene::origin_bound)
 hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int32_t* refs_in, int64_t n,
-                          float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res, hipStream_t st);
+                          float pad_abs, float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
+                          hipStream_t st);
 
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel
 

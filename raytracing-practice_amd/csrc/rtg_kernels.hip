@@ -33,6 +33,15 @@ namespace rtg {
 namespace {
 
 constexpr float kTMin = 0.001f;  // interval(0.001, infinity), camera.hpp:192
+// Conservative culling. Box tests only prune: a child is skipped when
+// its entry distance is past fmaf(tbest, kCullRel, kCullAbs) or its exit before kCullTMin, a margin at
+// least the oracle's (oracle/cpu_ref.c node_hit32: tbest (1 + 1e-6) + 1e-6, floor 0.0009), while the
+// primitive tests keep the exact tbest and tmin. With the boxes padded on the host for the slab test's
+// rounding (rtg_api.cpp pad_down), a box holding the closest hit is never culled by fp32 error.
+constexpr float kCullTMin = 0.0009f;
+constexpr float kCullRel = 1.0f + 0x1p-19f;
+constexpr float kCullAbs = 0x1p-19f;
+__device__ __forceinline__ float cull_bound(float tbest) { return fmaf(tbest, kCullRel, kCullAbs); }
 constexpr float kPi = 3.14159265358979323846f;
 constexpr int kMaxTexNesting = 16;
 
@@ -213,11 +222,11 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
-  // roots strictly inside (tmin, tmax), interval::surrounds (sphere.hpp:70): a sphere never replaces an
-  // equal-t hit (the tie rule)
-  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
-  if (tmin < lo && lo < tmax) return lo;
-  if (tmin < hi && hi < tmax) return hi;
+  // roots in (tmin, tmax]: strictly above tmin (interval::surrounds, sphere.hpp:70); a root equal to tmax
+  // is returned for the exact-t tie rule to decide (sphere_wins_tie; round 5)
+  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
+  if (tmin < lo && lo <= tmax) return lo;
+  if (tmin < hi && hi <= tmax) return hi;
   return -1.0f;
 }
 
@@ -258,20 +267,25 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // Exact-t ties (rtg-f32 spec, DESIGN.md §4 "tie rule"). The reference tests the world's objects in
 // list order (hittable_list.hpp:40-64) against a shrinking interval: quad::hit accepts t ==
 // closest_so_far (interval::contains, quad.hpp:62, interval.hpp:29), sphere::hit does not
-// (interval::surrounds, sphere.hpp:70, interval.hpp:32). So at equal t it keeps any quad over any
-// sphere and the later of two quads, whatever order they are tested in. The kernels test in BVH
-// order: sphere_t takes roots strictly below tmax (a sphere never replaces an equal-t hit), quad_t
-// roots up to tmax, and a quad root equal to the closest hit replaces it only if that hit is a sphere
-// or an earlier quad of the list (S.tie_rank: each quad slot's list index, read only on a tie; the
-// check is one compare and a wave-uniform branch). Two spheres at the bit-identical t (duplicate
-// spheres, a ray through a tangent point) keep the one tested first: the one order-dependent case,
-// left out of the rule because its compare cost config 2 3 %.
+// (interval::surrounds, sphere.hpp:70, interval.hpp:32). So among the primitives at the smallest t it
+// keeps the last quad of the list if there is one, else the first sphere, whatever order they are tested
+// in. The kernels test in BVH order: sphere_t and quad_t return roots up to tmax; a quad root equal to the
+// closest hit replaces it only if that hit is a sphere or an earlier quad of the list, a sphere root equal
+// to it only if that hit is a later sphere (round 5: duplicate spheres, a ray through a tangent point).
+// S.tie_rank holds each sphere / quad slot's list index and is read only on a tie: the check is one
+// compare and a wave-uniform branch that is almost never taken.
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
   if (!(best & kQuadRefBit)) return true;
   return qrank > S.tie_rank[S.num_spheres + (best & ~kQuadRefBit)];
+}
+// A sphere (slot `slot`) whose root equals the closest hit `best` (a primitive ref): it takes the hit only
+// from a sphere later in the list (every schedule; S.tie_rank lives in HBM, read only here).
+__device__ __forceinline__ bool sphere_wins_tie(const DevScene& S, int32_t slot, int32_t best) {
+  if (best < 0 || (best & kQuadRefBit)) return false;
+  return S.tie_rank[slot] < S.tie_rank[best];
 }
 
 template <bool COUNT>
@@ -408,10 +422,11 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, const Stk&
   const float r0x = fmaf(b.z, inv.x, oi.x), r1x = fmaf(c.y, inv.x, oi.x);
   const float r0y = fmaf(b.w, inv.y, oi.y), r1y = fmaf(c.z, inv.y, oi.y);
   const float r0z = fmaf(c.x, inv.z, oi.z), r1z = fmaf(c.w, inv.z, oi.z);
-  const float ln = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), kTMin));
-  const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), t.tbest));
-  const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kTMin));
-  const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), t.tbest));
+  const float tc = cull_bound(t.tbest);
+  const float ln = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), kCullTMin));
+  const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tc));
+  const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kCullTMin));
+  const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tc));
   // An empty slot (right child only; the host guarantees the left one is never empty) has an
   // inverted box, which the symmetric min/max slab form would report as all of space: test
   // the child code explicitly.
@@ -446,11 +461,12 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 
 // Entry distance of one child (tn) or a miss: the slab test with the near/far planes already
 // chosen by the ray's direction signs, so no min/max between a slab's two planes is needed.
+// tc: the cull bound of the closest hit so far (cull_bound)
 __device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, float tfx, float tfy,
-                                              float tfz, float tbest, uint32_t slot) {
-  const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kTMin);
-  const float tf = fminf(fminf(fminf(tfx, tfy), tfz), tbest);
-  // tn >= kTMin > 0, so its bits order like the float; the low 4 bits carry the slot (x4)
+                                              float tfz, float tc, uint32_t slot) {
+  const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kCullTMin);
+  const float tf = fminf(fminf(fminf(tfx, tfy), tfz), tc);
+  // tn >= kCullTMin > 0, so its bits order like the float; the low 4 bits carry the slot (x4)
   return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
 
@@ -531,10 +547,11 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   const f2 fx01 = pk_fma(f2{fx.x, fx.y}, ix, ox), fx23 = pk_fma(f2{fx.z, fx.w}, ix, ox);
   const f2 fy01 = pk_fma(f2{fy.x, fy.y}, iy, oy), fy23 = pk_fma(f2{fy.z, fy.w}, iy, oy);
   const f2 fz01 = pk_fma(f2{fz.x, fz.y}, iz, oz), fz23 = pk_fma(f2{fz.z, fz.w}, iz, oz);
-  uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, t.tbest, 0);
-  uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, t.tbest, 4);
-  uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, t.tbest, 8);
-  uint32_t k3 = child_key(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, t.tbest, 12);
+  const float tc = cull_bound(t.tbest);
+  uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tc, 0);
+  uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tc, 4);
+  uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tc, 8);
+  uint32_t k3 = child_key(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tc, 12);
   if constexpr (PAIRS) {
     // scene in global memory: the codes travel with their keys through the network, so no second
     // memory round trip sits between the sort and the next node load (-3.6 % on config 5; with
@@ -605,7 +622,9 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
-      if (th > 0.0f) {
+      bool take = th > 0.0f;
+      if (ballot_tie(take && th == t.tbest) != 0 && take && th == t.tbest) take = sphere_wins_tie(S, first + k, t.best);
+      if (take) {
         t.tbest = th;
         t.best = first + k;
         t.mat = MAT ? ibits(sp4[1].w) : -1;
@@ -636,7 +655,8 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
-      take = th > 0.0f;  // sphere_t: th < tbest
+      take = th > 0.0f;
+      if (ballot_tie(take && th == t.tbest) != 0 && take && th == t.tbest) take = sphere_wins_tie(S, ref, t.best);
     }
     if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
@@ -1762,6 +1782,34 @@ bool dual_fits_registers(bool count, bool ring, bool verbose) {
   if (verbose) std::fprintf(stderr, "[rtg] dual check: numRegs %d\n", r.vgprs);
   if (!r.ok) return false;
   return 5 * ((r.vgprs + 7) / 8 * 8) <= 512;
+}
+
+// Widen the culling margin of a node array in place (a camera farther out than the origin bound the boxes
+// were padded for, rtg_api.cpp ensure_origin_bound): every finite box plane moves outward by delta (+ a
+// 2^-22 |v| guard for this subtraction's own rounding); codes and empty slots (+-inf) are left alone.
+// width 4: 28 floats per node (12 lo, 12 hi, 4 codes); width 2: 16 (lo, hi, lo, hi, 4 codes).
+__global__ __launch_bounds__(256) void repad_nodes_kernel(float* __restrict__ nodes, int64_t n_floats, int width,
+                                                          float delta) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n_floats) return;
+  const int w = static_cast<int>(k % (width == 4 ? 28 : 16));
+  int side;  // -1 lo plane, +1 hi plane, 0 code
+  if (width == 4)
+    side = w < 12 ? -1 : (w < 24 ? 1 : 0);
+  else
+    side = w < 12 ? ((w % 6) < 3 ? -1 : 1) : 0;
+  const float v = nodes[k];
+  if (side == 0 || !(fabsf(v) < __builtin_inff())) return;
+  const float g = delta + fabsf(v) * 0x1p-22f;
+  nodes[k] = side < 0 ? v - g : v + g;
+}
+
+hipError_t launch_repad(float* nodes, int64_t num_nodes, int width, float delta, hipStream_t stream) {
+  const int64_t n = num_nodes * (width == 4 ? 28 : 16);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(repad_nodes_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, nodes,
+                     n, width, delta);
+  return hipGetLastError();
 }
 
 hipError_t launch_combine(const float* partial, float* out, int64_t n_pixels, int chunks, float scale,

@@ -187,7 +187,8 @@ class Library:
     """librtgpu.so. Loading it requires the built library (make -C raytracing-practice_amd)."""
 
     def __init__(self, path: Optional[str] = None):
-        path = path or os.path.join(LIB_DIR, "librtgpu.so")
+        # RTGPU_LIB: an alternative build of the library (same-box A/B runs, tools/); default the in-tree one
+        path = path or os.environ.get("RTGPU_LIB") or os.path.join(LIB_DIR, "librtgpu.so")
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} not built (run __graft_entry__.build())")
         self.path = path

@@ -625,6 +625,50 @@ def test_exact_t_ties_match_oracle(gpu_lib, oracle, bvh):
     assert n[GREEN] > 200 and n[BLUE] > 100 and n[RED] == 0 and n[WHITE] == 0, n
 
 
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
+def test_sphere_ties_follow_list_order(gpu_lib, oracle, bvh):
+    """The exact-t tie rule for spheres: groups of three identical
+    spheres hit at bit-identical t, listed so that each group's first member is last in some builders'
+    leaf order. Whatever order a BVH tests them in, the frame is cpu_ref32's bit for bit and equals the
+    frame of the scene that holds only each group's first member (sphere::hit never replaces an equal-t
+    hit, sphere.hpp:70, so the reference's list walk keeps the first)."""
+    from tie_scene import duplicate_sphere_scene
+
+    d, cam = duplicate_sphere_scene(bvh, width=96)
+    ds = gpu_lib.scene_create(d)
+    g, st = ds.render_host(cam)
+    ds.close()
+    o, segs = oracle.render_f32(d, cam)
+    assert np.array_equal(g, o) and st.segments == segs
+    d1, _ = duplicate_sphere_scene(bvh, width=96, dedup=True)
+    ds = gpu_lib.scene_create(d1)
+    g1, st1 = ds.render_host(cam)
+    ds.close()
+    assert np.array_equal(g, g1) and st.segments == st1.segments
+
+
+@pytest.mark.parametrize("competitor", ["quad", "sphere"])
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
+def test_near_tie_culling_is_conservative(gpu_lib, oracle, bvh, competitor):
+    """Conservative BVH culling: small spheres whose tops poke a
+    fraction of an fp32 ulp above a quad or a large sphere at y = 1000, seen from just above. The
+    competitor is tested first and its hit lies within the slab test's rounding of the small sphere's box
+    entry; with the host-padded boxes and the tbest margin the kernel still enters that box, so the frame
+    and the segment count are cpu_ref32's (which culls in f64 with a margin) bit for bit, for every BVH
+    builder. The camera lies above the scene's primitive bounds, so the render also widens the margin
+    (ensure_origin_bound); a second camera 100 units up widens it again."""
+    from tie_scene import GREEN, colour_counts, near_tie_scene
+
+    for h in (2.0, 100.0):
+        d, cam = near_tie_scene(bvh, competitor, width=96, cam_height=h)
+        ds = gpu_lib.scene_create(d)
+        g, st = ds.render_host(cam)
+        ds.close()
+        o, segs = oracle.render_f32(d, cam)
+        assert colour_counts(o)[GREEN] > 500, h
+        assert np.array_equal(g, o) and st.segments == segs, (h, colour_counts(g), colour_counts(o))
+
+
 def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypatch):
     """Deep BVHs keep the first stack entries in LDS and the rest in a global per-wave spill area
     (the 1M-sphere scene needs 36 entries). RTG_STACK_LDS_ENTRIES lowers the LDS part so that the

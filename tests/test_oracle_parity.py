@@ -216,3 +216,24 @@ def test_exact_t_ties_follow_reference_list_order(oracle):
         n = colour_counts(frame)
         assert n[GREEN] > 50 and n[BLUE] > 30, n  # the last quad; the sphere beside them
         assert n[RED] == 0 and n[WHITE] == 0, n
+
+
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_MEDIAN])
+def test_oracle_sphere_ties_follow_list_order(oracle, bvh):
+    """cpu_ref32's exact-t tie rule for spheres (round 5): groups of three identical spheres show their
+    first list member, as the reference's list walk does (sphere::hit rejects t == closest_so_far,
+    sphere.hpp:70): the frame equals the frame of the scene holding only those first members."""
+    from tie_scene import GREEN, WHITE, colour_counts, duplicate_sphere_scene, near_tie_scene
+
+    d, cam = duplicate_sphere_scene(bvh, width=48)
+    f, segs = oracle.render_f32(d, cam)
+    d1, _ = duplicate_sphere_scene(bvh, width=48, dedup=True)
+    f1, segs1 = oracle.render_f32(d1, cam)
+    assert np.array_equal(f, f1) and segs == segs1
+    # the near-tie scene (conservative culling, DESIGN.md §4): the oracle sees the small sphere that pokes
+    # a fraction of an ulp above the competitor on the apex disc, the competitor around it
+    for comp in ("quad", "sphere"):
+        d, cam = near_tie_scene(bvh, comp, width=32)
+        f, _ = oracle.render_f32(d, cam)
+        n = colour_counts(f)
+        assert n[GREEN] > 100 and n[WHITE] > 300, (comp, n)

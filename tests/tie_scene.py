@@ -49,3 +49,79 @@ def C_arr(c):
     import numpy as np
 
     return np.array(c, dtype=np.float32)
+
+
+def make_desc(prims, mats, texs, bvh_mode):
+    P = (rtgpu.rtg_primitive * len(prims))(*prims)
+    M = (rtgpu.rtg_material * len(mats))(*mats)
+    T = (rtgpu.rtg_texture * len(texs))(*texs)
+    d = rtgpu.rtg_scene_desc(abi_version=rtgpu.RTG_ABI_VERSION, bvh_mode=bvh_mode,
+                             prims=C.cast(P, C.POINTER(rtgpu.rtg_primitive)), num_prims=len(prims),
+                             materials=C.cast(M, C.POINTER(rtgpu.rtg_material)), num_materials=len(mats),
+                             textures=C.cast(T, C.POINTER(rtgpu.rtg_texture)), num_textures=len(texs))
+    d._keep = (P, M, T)
+    return d
+
+
+def _sphere(m, c, r):
+    return rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_SPHERE, material=m, p0=rtgpu.D3(*c), p1=rtgpu.D3(*c),
+                               radius=r)
+
+
+def _lights(cols):
+    tex = [rtgpu.rtg_texture(type=rtgpu.RTG_TEX_SOLID, color=rtgpu.D3(*c)) for c in cols]
+    mat = [rtgpu.rtg_material(type=rtgpu.RTG_MAT_DIFFUSE_LIGHT, texture=k) for k in range(len(cols))]
+    return mat, tex
+
+
+def duplicate_sphere_scene(bvh_mode=rtgpu.RTG_BVH_SAH, width=64, dedup=False):
+    """Sphere-sphere exact-t ties (DESIGN.md §4 "tie rule", round 5): a 4x4 grid of groups of three
+    identical spheres (emitting red, green, blue), every ray that reaches a group hits its three spheres at
+    bit-identical t. The list holds every group's first member, then every second, then every third, with
+    the colours rotated per group; sphere::hit never replaces an equal-t hit (interval::surrounds,
+    sphere.hpp:70), so the reference's list walk (hittable_list.hpp:40-64) shows each group's FIRST
+    member. dedup=True: the same scene with only those first members (the expected image)."""
+    cols = [RED, GREEN, BLUE]
+    mat, tex = _lights(cols)
+    groups = [(-4.5 + 3.0 * (g % 4), -4.5 + 3.0 * (g // 4)) for g in range(16)]
+    prims = []
+    for member in range(1 if dedup else 3):
+        for g, (x, y) in enumerate(groups):
+            prims.append(_sphere((g + member) % 3, (x, y, 0.0), 1.2))
+    cam = rtgpu.camera(image_width=width, aspect_ratio=1.0, samples_per_pixel=4, max_depth=3,
+                       background=(0.0, 0.0, 0.0), lookfrom=(0.3, 0.2, 20.0), lookat=(0, 0, 0), vfov=36.0)
+    return make_desc(prims, mat, tex, bvh_mode), cam
+
+
+# near-tie height: the competitor's surface at Y0, the small spheres' tops a fraction of an fp32 ulp above it
+NEAR_TIE_Y0 = 1000.0
+
+
+def near_tie_scene(bvh_mode=rtgpu.RTG_BVH_SAH, competitor="quad", width=64, cam_height=2.0):
+    """Near ties for the BVH culling margin (DESIGN.md §4 "conservative culling"): a
+    3x3 field of small spheres (centre y = 999.5, radius 0.5 + j 2^-21, j = 1..3) whose tops poke 1/64 ..
+    3/64 of an fp32 ulp above a competitor surface at y = 1000 (a large quad, or a sphere of radius 1000
+    below it), far from the world origin. A ray from just above an apex hits the small sphere at its box's
+    top face a little before the competitor, which is tested first (its box is entered first, or it is the
+    scene-spanning occluder); the fp32 slab test's rounding, about 2^-24 |o| / |d|, is ~60x that gap here,
+    so a culling bound without the host padding and the tbest margin culls the box that holds the closest
+    hit. The camera sits above the centre apex, zoomed in on it."""
+    import numpy as np
+
+    mat, tex = _lights([RED, GREEN, BLUE, WHITE])
+    y0 = NEAR_TIE_Y0
+    prims = []
+    if competitor == "quad":
+        prims.append(rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_QUAD, material=3, p0=rtgpu.D3(-8.0, y0, -8.0),
+                                         p1=rtgpu.D3(16.0, 0.0, 0.0), p2=rtgpu.D3(0.0, 0.0, 16.0)))
+    else:
+        prims.append(_sphere(3, (0.0, y0 - 1000.0, 0.0), 1000.0))
+    for g in range(9):
+        x, z = -4.0 + 4.0 * (g % 3), -4.0 + 4.0 * (g // 3)
+        prims.append(_sphere(g % 3, (x, y0 - 0.5, z), 0.5 + (1 + g % 3) * 2.0 ** -21))
+    half = 1.5e-3  # the apex discs poking above y0 have radii 0.7e-3 .. 1.2e-3
+    cam = rtgpu.camera(image_width=width, aspect_ratio=1.0, samples_per_pixel=4, max_depth=3,
+                       background=(0.0, 0.0, 0.0), lookfrom=(0.0, y0 + cam_height, 0.0),
+                       lookat=(0.0, y0, 0.0), vup=(0.0, 0.0, 1.0),
+                       vfov=float(np.degrees(2 * np.arctan(half / cam_height))), focus_dist=cam_height)
+    return make_desc(prims, mat, tex, bvh_mode), cam

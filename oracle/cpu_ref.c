@@ -1141,8 +1141,55 @@ static f3 sample32(const world32* w, const rtg_camera_desc* cam, const float* cf
 }
 
 /* cpu_ref32 render: rows row_begin + k*row_stride, k < row_count; out = scale * sum (fp32). */
-int orc_render_f32(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint64_t seed, int row_begin,
-                   int row_stride, int row_count, float* out, uint64_t* segments) {
+/* rows r = r0, r0 + rstep, ... < row_count of the shard (image row row_begin + r * row_stride) */
+typedef struct {
+  const world32* w;
+  const rtg_camera_desc* cam;
+  const float* cf;
+  const rtg_camera_params* cp;
+  uint64_t seed;
+  int row_begin, row_stride, row_count, r0, rstep;
+  float* out;
+  uint64_t segs;
+} rows32_arg;
+
+static void* render_rows32(void* p) {
+  rows32_arg* a = (rows32_arg*)p;
+  const rtg_camera_params* cp = a->cp;
+  const rtg_camera_desc* cam = a->cam;
+  const float scale = (float)cp->pixel_samples_scale;
+  uint64_t segs = 0;
+  for (int r = a->r0; r < a->row_count; r += a->rstep) {
+    int j = a->row_begin + r * a->row_stride;
+    for (int i = 0; i < cp->image_width; ++i) {
+      uint32_t pid = (uint32_t)j * (uint32_t)cp->image_width + (uint32_t)i;
+      /* rtg-f32 accumulation (rtgpu.h rtg_chunk_samples): chunks of K samples summed from zero in
+         sample order, chunk sums added in chunk order; one chunk == the reference's running sum */
+      f3 acc = F3(0.0f, 0.0f, 0.0f);
+      if (cam->max_depth > 0) {
+        int spp = cam->samples_per_pixel, K = rtg_chunk_samples(spp);
+        for (int c0 = 0; c0 < spp; c0 += K) {
+          f3 part = F3(0.0f, 0.0f, 0.0f);
+          for (int smp = c0; smp < spp && smp < c0 + K; ++smp)
+            part = fv_add(part, sample32(a->w, cam, a->cf, a->seed, pid, (uint32_t)smp, i, j, &segs));
+          acc = c0 == 0 ? part : fv_add(acc, part);
+        }
+      }
+      float* o = a->out + ((int64_t)r * cp->image_width + i) * 3;
+      o[0] = scale * acc.x;
+      o[1] = scale * acc.y;
+      o[2] = scale * acc.z;
+    }
+  }
+  a->segs = segs;
+  return 0;
+}
+
+/* cpu_ref32 over rows row_begin + k * row_stride, k < row_count, on `threads` threads sharing one world
+   (rows dealt round-robin; every pixel's arithmetic is the single-threaded one, so the frame does not
+   depend on the thread count). threads <= 1: the caller's thread only. */
+int orc_render_f32_mt(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint64_t seed, int row_begin,
+                      int row_stride, int row_count, float* out, uint64_t* segments, int threads) {
   rtg_camera_params cp;
   orc_camera_resolve(cam, &cp);
   if (row_stride < 1) row_stride = 1;
@@ -1157,35 +1204,33 @@ int orc_render_f32(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint64_t
     cf[15 + k] = (float)cp.defocus_disk_v[k];
     cf[18 + k] = (float)cam->background[k];
   }
-  float scale = (float)cp.pixel_samples_scale;
   world32 w;
   world32_init(&w, s);
-  uint64_t segs = 0;
-  for (int r = 0; r < row_count; ++r) {
-    int j = row_begin + r * row_stride;
-    for (int i = 0; i < cp.image_width; ++i) {
-      uint32_t pid = (uint32_t)j * (uint32_t)cp.image_width + (uint32_t)i;
-      /* rtg-f32 accumulation (rtgpu.h rtg_chunk_samples): chunks of K samples summed from zero in
-         sample order, chunk sums added in chunk order; one chunk == the reference's running sum */
-      f3 acc = F3(0.0f, 0.0f, 0.0f);
-      if (cam->max_depth > 0) {
-        int spp = cam->samples_per_pixel, K = rtg_chunk_samples(spp);
-        for (int c0 = 0; c0 < spp; c0 += K) {
-          f3 part = F3(0.0f, 0.0f, 0.0f);
-          for (int smp = c0; smp < spp && smp < c0 + K; ++smp)
-            part = fv_add(part, sample32(&w, cam, cf, seed, pid, (uint32_t)smp, i, j, &segs));
-          acc = c0 == 0 ? part : fv_add(acc, part);
-        }
-      }
-      float* o = out + ((int64_t)r * cp.image_width + i) * 3;
-      o[0] = scale * acc.x;
-      o[1] = scale * acc.y;
-      o[2] = scale * acc.z;
-    }
+  if (threads < 1) threads = 1;
+  if (threads > row_count) threads = row_count > 0 ? row_count : 1;
+  rows32_arg* args = (rows32_arg*)calloc(threads, sizeof(rows32_arg));
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  for (int k = 0; k < threads; ++k) {
+    rows32_arg a = {&w, cam, cf, &cp, seed, row_begin, row_stride, row_count, k, threads, out, 0};
+    args[k] = a;
+    if (k > 0) pthread_create(&th[k], 0, render_rows32, &args[k]);
+  }
+  render_rows32(&args[0]);
+  uint64_t segs = args[0].segs;
+  for (int k = 1; k < threads; ++k) {
+    pthread_join(th[k], 0);
+    segs += args[k].segs;
   }
   if (segments) *segments = segs;
+  free(th);
+  free(args);
   world32_free(&w);
   return 0;
+}
+
+int orc_render_f32(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint64_t seed, int row_begin,
+                   int row_stride, int row_count, float* out, uint64_t* segments) {
+  return orc_render_f32_mt(s, cam, seed, row_begin, row_stride, row_count, out, segments, 1);
 }
 
 /* write_color (color.hpp:14-58) on a double pixel: the reference's byte triple */

@@ -21,6 +21,8 @@ class Oracle:
         L.orc_camera_resolve.argtypes = [P(rtgpu.rtg_camera_desc), P(rtgpu.rtg_camera_params)]
         L.orc_render_f32.argtypes = [P(rtgpu.rtg_scene_desc), P(rtgpu.rtg_camera_desc), C.c_uint64,
                                      C.c_int, C.c_int, C.c_int, C.c_void_p, P(C.c_uint64)]
+        L.orc_render_f32_mt.argtypes = [P(rtgpu.rtg_scene_desc), P(rtgpu.rtg_camera_desc), C.c_uint64,
+                                        C.c_int, C.c_int, C.c_int, C.c_void_p, P(C.c_uint64), C.c_int]
         L.orc_render_f64.argtypes = [P(rtgpu.rtg_scene_desc), P(rtgpu.rtg_camera_desc), C.c_uint,
                                      C.c_int, C.c_int, C.c_void_p, P(C.c_uint64)]
         L.orc_bench_f64.argtypes = [P(rtgpu.rtg_scene_desc), P(rtgpu.rtg_camera_desc), C.c_int,
@@ -84,13 +86,15 @@ class Oracle:
         self.lib.orc_camera_resolve(C.byref(cam), C.byref(out))
         return out
 
-    def render_f32(self, desc, cam, seed=rtgpu.DEFAULT_SEED, row_begin=0, row_stride=1, row_count=0):
+    def render_f32(self, desc, cam, seed=rtgpu.DEFAULT_SEED, row_begin=0, row_stride=1, row_count=0, threads=1):
+        """cpu_ref32 rows (threads > 1: one shared world, rows dealt over that many threads; the frame
+        does not depend on it)."""
         p = self.camera_resolve(cam)
         rows = row_count if row_count > 0 else (p.image_height - 1 - row_begin) // row_stride + 1
         out = np.zeros((rows, p.image_width, 3), dtype=np.float32)
         segs = C.c_uint64(0)
-        self.lib.orc_render_f32(C.byref(desc), C.byref(cam), seed, row_begin, row_stride, rows,
-                                out.ctypes.data, C.byref(segs))
+        self.lib.orc_render_f32_mt(C.byref(desc), C.byref(cam), seed, row_begin, row_stride, rows,
+                                   out.ctypes.data, C.byref(segs), threads)
         return out, segs.value
 
     def render_f64(self, desc, cam, seed=1, row_begin=0, row_count=0):

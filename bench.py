@@ -69,9 +69,9 @@ def parse():
     ap.add_argument("--gather", choices=["f32", "rgb8"], default="f32",
                     help="gather the linear fp32 frame (default) or the write_color bytes (4x fewer)")
     ap.add_argument("--gather-impl", choices=["rtg", "torch"], default="torch",
-                    help="N>1 timed gather: torch.distributed.gather + a torch de-interleave (default until the "
-                         "C-ABI path has run on a multi-GPU node) or the C-ABI's RCCL gather + de-interleave "
-                         "kernel (rtg_gather_rows)")
+                    help="N>1 timed gather: torch.distributed.gather into blocks allocated once + the library's "
+                         "de-interleave kernel (rtgpu.FrameGather; default until the C-ABI path has run on a "
+                         "multi-GPU node) or the C-ABI's RCCL gather + de-interleave kernel (rtg_gather_rows)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="N>1 process group: nccl (= RCCL, one rank per GPU) or gloo (rehearsal of the N>1 flow "
                          "with several ranks on one GPU; the frame is gathered through host memory)")
@@ -386,6 +386,15 @@ def main():
                                 device="cuda")
     ev_g0, ev_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     gathered = [None]  # the last gathered frame (rank 0, N > 1)
+    # --gather-impl torch: every buffer of the timed gather allocated here, once (rtgpu.FrameGather: the
+    # staging blocks and the frame on rank 0, the de-interleave by the library's own kernel); gloo
+    # rehearsals stage the shard through one pinned host buffer
+    fgather, host_src = None, None
+    if world > 1 and comm is None:
+        gsrc = shard8 if shard8 is not None else shard
+        if gloo:
+            host_src = torch.empty(gsrc.shape, dtype=gsrc.dtype, pin_memory=True)
+        fgather = rtgpu.FrameGather(lib, host_src if gloo else gsrc, H, dst=0, device=local)
 
     def step(i, evs=None):
         # a rank past the image's last row renders nothing (its shard stays zero padding)
@@ -401,8 +410,11 @@ def main():
                 comm.gather_rows([src.data_ptr()], H, W * 3 * src.element_size(), 0,
                                  frame.data_ptr() if frame is not None else 0, [stream])
                 gathered[0] = frame
+            elif gloo:
+                host_src.copy_(src)
+                gathered[0] = fgather(host_src)
             else:
-                gathered[0] = rtgpu.gather_frame(src.cpu() if gloo else src, H)
+                gathered[0] = fgather(src, stream)
             g1.record()
         return st
 

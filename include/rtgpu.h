@@ -304,7 +304,10 @@ typedef struct rtg_launch_plan {
   int32_t ray_queue;         /* always 0 since round 5 (the RTG_RAY_QUEUE prototype was retired to
                                 tools/experiments/ray_queue.patch); the word keeps the layout */
   int32_t node_width;        /* BVH node width the kernels traverse: 2 (RTG_BVH_MEDIAN) or 4 */
-  int32_t reserved_[1];
+  /* round 5, layout-compatible (ABI 5's last reserved word): M of the conservative culling margin, rounded
+     up: the node boxes are padded for ray origins with |coordinate| <= 2M; a render whose
+     camera reaches farther raises it (and the padding) first */
+  int32_t origin_bound;
 } rtg_launch_plan;
 
 rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,

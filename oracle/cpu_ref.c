@@ -861,6 +861,24 @@ static void world32_init(world32* w, const rtg_scene_desc* s) {
     for (int i = 0; i < 256; ++i)
       for (int a = 0; a < 3; ++a) w->pvec[k * 768 + i * 3 + a] = (float)s->perlins[k].randvec[i][a];
 }
+/* The spec's closest hit is over every primitive by the fp32 tests (with the tie rule); the BVH only
+   prunes. The reference's exact f64 boxes can prune a hit the fp32 tests accept: a point the fp32 quad
+   test puts inside an edge, or a ray the fp32 sphere discriminant lets graze a box face. So cpu_ref32 tests
+   its (f64) boxes padded by 2^-18 (|plane| + M), M the largest |coordinate| of the scene and the camera:
+   far beyond both the fp32 tests' acceptance error and the kernels' own margin (DESIGN.md §4
+   "conservative culling"), so neither side's culling decides a pixel. cpu_ref64 keeps the reference's
+   boxes as they are. */
+static void world32_pad(world32* w, double cam_bound) {
+  if (w->bvh.n <= 0) return;
+  double m = cam_bound;
+  for (int a = 0; a < 3; ++a) m = fmax(m, fmax(fabs(w->bvh.nodes[0].box.lo[a]), fabs(w->bvh.nodes[0].box.hi[a])));
+  for (int64_t k = 0; k < w->bvh.n; ++k)
+    for (int a = 0; a < 3; ++a) {
+      obox* b = &w->bvh.nodes[k].box;
+      b->lo[a] -= 0x1p-18 * (fabs(b->lo[a]) + m);
+      b->hi[a] += 0x1p-18 * (fabs(b->hi[a]) + m);
+    }
+}
 static void world32_free(world32* w) {
   free(w->bvh.nodes);
   free(w->sph);
@@ -1206,6 +1224,10 @@ int orc_render_f32_mt(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint6
   }
   world32 w;
   world32_init(&w, s);
+  double cam_bound = 0.0;
+  for (int a = 0; a < 3; ++a)
+    cam_bound = fmax(cam_bound, fabs(cp.center[a]) + fabs(cp.defocus_disk_u[a]) + fabs(cp.defocus_disk_v[a]));
+  world32_pad(&w, cam_bound);
   if (threads < 1) threads = 1;
   if (threads > row_count) threads = row_count > 0 ? row_count : 1;
   rows32_arg* args = (rows32_arg*)calloc(threads, sizeof(rows32_arg));

@@ -125,11 +125,14 @@ float round_up(double x) {
   return f;
 }
 // Culling margin (DESIGN.md §4 "conservative culling"): every BVH box plane the kernels test is moved
-// outward by eta = 2^-21 (|plane| + M) before its fp32 rounding (itself outward), where M bounds
-// |coordinate| of every ray origin (primitive boxes, the camera). The kernels' slab test
-// fma(plane, rcp(d), -o rcp(d)) errs by at most 3 2^-24 |plane - o| + 2^-24 |o| in world units along
-// the axis (v_rcp_f32: 1 ulp), i.e. < eta / 2: a computed entry (exit) distance is then never past the
-// unpadded box's true one, so no box holding a primitive hit is culled by rounding.
+// outward by eta = 2^-21 (|plane| + M) before its fp32 rounding (itself outward), where M is the largest
+// |coordinate| of the primitive boxes (so of every hit point a segment starts from). The kernels' slab test
+// fma(plane, rcp(d), -o rcp(d)) errs by at most 3 2^-24 |plane - o| + 2^-24 |o| <= 2^-22 (|plane| + |o|)
+// in world units along the axis (v_rcp_f32: 1 ulp), i.e. <= eta / 2 for every origin with |o| <= M and
+// <= eta for |o| <= 2M (a camera up to twice the scene's reach; ensure_origin_bound widens the pad for one
+// farther out): a computed entry (exit) distance is never past the unpadded box's true one, so no box that
+// holds a primitive hit is culled by rounding; the rest of eta covers the fp32
+// primitive tests' acceptance error (a point the quad test puts inside an edge).
 float pad_down(double lo, double m) {
   return std::isfinite(lo) ? round_down(lo - 0x1p-21 * (std::fabs(lo) + m)) : static_cast<float>(lo);
 }
@@ -1483,10 +1486,10 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   return RTG_OK;
 }
 
-// The culling margin covers ray origins with |coordinate| <= s->origin_bound (the primitive boxes when the
-// scene was created). A camera whose lens reaches farther out widens the pad of every node box on the
-// device first (repad_nodes_kernel, on the render's stream; 1/16 headroom so a camera moving about does
-// not repad every frame). Boxes only grow: frames are unchanged, the conservative bound holds again.
+// The culling margin covers ray origins with |coordinate| <= 2 s->origin_bound (pad_down: M = the primitive
+// boxes' reach when the scene was created). A camera whose lens reaches farther out widens the pad of every
+// node box on the device first (repad_nodes_kernel, on the render's stream; 1/16 headroom so a camera moving
+// about does not repad every frame). Boxes only grow: frames are unchanged, the bound holds again.
 rtg_status ensure_origin_bound(rtg_scene* s, const rtg_camera_desc* cam, hipStream_t stream) {
   if (s->dev.num_nodes <= 0) return RTG_OK;
   rtg_camera_params cp;
@@ -1494,9 +1497,9 @@ rtg_status ensure_origin_bound(rtg_scene* s, const rtg_camera_desc* cam, hipStre
   double mc = 0.0;
   for (int a = 0; a < 3; ++a)
     mc = std::max(mc, std::fabs(cp.center[a]) + std::fabs(cp.defocus_disk_u[a]) + std::fabs(cp.defocus_disk_v[a]));
-  if (mc <= s->origin_bound) return RTG_OK;
+  if (mc <= 2.0 * s->origin_bound) return RTG_OK;
   if (!(mc < 1e30)) return fail(RTG_E_INVALID, "camera position not finite (or above 1e30)");
-  const double target = mc * (1.0 + 1.0 / 16.0);
+  const double target = 0.5 * mc * (1.0 + 1.0 / 16.0);
   const float delta = round_up(0x1p-21 * (target - s->origin_bound));
   RTG_HIP(launch_repad(reinterpret_cast<float*>(const_cast<float4*>(s->dev.nodes)), s->dev.num_nodes,
                        s->dev.node_width, delta, stream),
@@ -1549,6 +1552,7 @@ rtg_status rtg_render_plan(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
   out->tile_slots = P.ring_slots;
   out->num_cus = s->num_cus;
   out->ray_queue = 0;  // retired in round 5 (tools/experiments/ray_queue.patch)
+  out->origin_bound = static_cast<int32_t>(std::min(std::ceil(s->origin_bound), 2147483647.0));
   out->node_width = P.dscene.node_width;
   if (P.variant == 5) {
     out->treelet_hot = s->treelet_key == treelet_key(cam, job) ? 1 : 0;

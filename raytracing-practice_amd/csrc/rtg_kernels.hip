@@ -617,19 +617,38 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     t.todo = kTravDone;
     return;
   }
+  // Sphere ties (DESIGN.md §4 "tie rule") are settled per leaf, off the hot path: the loop takes only roots
+  // strictly below the closest hit and flags a lane whose sphere root equalled it; a flagged lane re-tests the
+  // leaf's spheres against the final closest hit and takes an equal root from a sphere earlier in the list
+  // (sphere_wins_tie). The rare branch runs once per leaf, not per sphere test (an inline check per sphere
+  // cost book-1 +2 % and the 1M field +7 % in register allocation, round 5).
+  bool tie = false;
+  auto settle_ties = [&](auto ref_of) {
+    if (ballot_tie(tie) == 0 || !tie) return;
+    for (int k = 0; k < count; ++k) {
+      const int32_t ref = ref_of(k);
+      if (ref & kQuadRefBit) continue;
+      const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
+      const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
+      if (th == t.tbest && sphere_wins_tie(S, ref, t.best)) {
+        t.best = ref;
+        t.mat = MAT ? ibits(sp4[1].w) : -1;
+      }
+    }
+  };
   if ((PRIMS & kPrimsKind) == kPrimsSpheres || ((PRIMS & kPrimsKind) == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
-      bool take = th > 0.0f;
-      if (ballot_tie(take && th == t.tbest) != 0 && take && th == t.tbest) take = sphere_wins_tie(S, first + k, t.best);
-      if (take) {
+      tie = tie || th == t.tbest;
+      if (th > 0.0f && th < t.tbest) {
         t.tbest = th;
         t.best = first + k;
         t.mat = MAT ? ibits(sp4[1].w) : -1;
       }
     }
+    settle_ties([&](int k) { return first + k; });
     pop();
     return;
   }
@@ -655,8 +674,8 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
-      take = th > 0.0f;
-      if (ballot_tie(take && th == t.tbest) != 0 && take && th == t.tbest) take = sphere_wins_tie(S, ref, t.best);
+      tie = tie || th == t.tbest;
+      take = th > 0.0f && th < t.tbest;
     }
     if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
@@ -664,6 +683,8 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       t.mat = MAT ? m : qrank;
     }
   }
+  if constexpr ((PRIMS & kPrimsKind) != kPrimsQuads)
+    settle_ties([&](int k) { return S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit); });
   pop();
 }
 

@@ -119,7 +119,7 @@ class rtg_launch_plan(C.Structure):
         "chunks")] + [("partial_bytes", C.c_int64), ("num_cus", C.c_int32), ("tile_slots", C.c_int32),
                       ("treelet_hot", C.c_int32), ("treelet_tune_us", C.c_int32),
                       ("treelet_visit_permille", C.c_int32), ("ray_queue", C.c_int32),
-                      ("node_width", C.c_int32), ("reserved_", C.c_int32 * 1)]
+                      ("node_width", C.c_int32), ("origin_bound", C.c_int32)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved_"}
@@ -614,3 +614,47 @@ def gather_frame(shard, height: int, dst: int = 0):
         return deinterleave(parts, height)
     dist.gather(shard, dst=dst)
     return None
+
+
+class FrameGather:
+    """The N > 1 frame gather of bench.py's timed loop, with every buffer allocated once.
+
+    Rank `dst` owns a staging tensor of N padded shard blocks (the rtg_gather_rows layout) and the
+    (height, W, C) frame; each call gathers every rank's shard into the blocks (torch.distributed.gather:
+    the RCCL gather under "nccl", gloo on CPU) and de-interleaves them with the library's own kernel
+    (rtg_deinterleave_rows on the shard's stream; its host twin rtg_deinterleave_rows_host for CPU
+    tensors), so a timed step allocates nothing. Returns the frame on dst (the same tensor every call) and
+    None elsewhere. The shard must keep its shape between calls."""
+
+    def __init__(self, lib: Library, shard, height: int, dst: int = 0, device: int = 0):
+        import torch.distributed as dist
+
+        self.lib, self.height, self.dst, self.device = lib, height, dst, device
+        self.world = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.shape = tuple(shard.shape)
+        self.row_bytes = int(shard[0].numel() * shard.element_size())
+        self.stage = self.parts = self.frame = None
+        if self.rank == dst:
+            self.stage = shard.new_empty((self.world,) + self.shape)
+            self.parts = list(self.stage.unbind(0))  # views into the staging blocks
+            self.frame = shard.new_empty((height,) + self.shape[1:])
+
+    def __call__(self, shard, stream_ptr: Optional[int] = None):
+        import torch.distributed as dist
+
+        assert tuple(shard.shape) == self.shape, "the shard changed shape after FrameGather was set up"
+        if self.world == 1:
+            return shard[: self.height]
+        if self.rank != self.dst:
+            dist.gather(shard, dst=self.dst)
+            return None
+        dist.gather(shard, gather_list=self.parts, dst=self.dst)
+        if self.stage.is_cuda:
+            self.lib.deinterleave_rows(self.device, self.stage.data_ptr(), self.frame.data_ptr(), self.world,
+                                       self.height, self.row_bytes, stream_ptr)
+        else:
+            self.lib.check("rtg_deinterleave_rows_host", self.lib.lib.rtg_deinterleave_rows_host(
+                C.c_void_p(self.stage.data_ptr()), C.c_void_p(self.frame.data_ptr()), self.world,
+                self.height, self.row_bytes))
+        return self.frame

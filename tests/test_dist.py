@@ -115,3 +115,57 @@ def test_bad_layout_arguments_are_rejected(lib):
     for args in ((0, 2, 0), (10, 0, 0), (10, 2, 2), (10, 2, -1)):
         with pytest.raises(rtgpu.RtgError):
             lib.shard_layout(*args)
+
+
+def _frame_gather_worker(rank, world, port, H, W, result_path):
+    """bench.py's timed N > 1 gather (rtgpu.FrameGather): buffers allocated once at set-up; a step —
+    gather into the staging blocks, the library's de-interleave — allocates no tensor (torch's
+    allocating factories are made to raise around the calls) and returns the same frame tensor."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import rtgpu
+
+        lib = rtgpu.Library()
+        b, stride, n, padded = lib.shard_layout(H, world, rank)
+        shard = torch.full((padded, W, 3), -1.0, dtype=torch.float32)
+        fg = rtgpu.FrameGather(lib, shard, H)
+
+        def boom(*a, **k):
+            raise AssertionError("tensor allocated inside a timed gather step")
+
+        names = ("empty", "zeros", "empty_like", "zeros_like", "cat", "stack")
+        saved = {k: getattr(torch, k) for k in names}
+        saved_new = torch.Tensor.new_empty
+        frames = []
+        for step in range(3):
+            if n:  # this step's pixel codes, offset per step
+                shard[:n] = torch.from_numpy(_pixel_codes([b + k * stride for k in range(n)], W) + step)
+            for k in names:
+                setattr(torch, k, boom)
+            torch.Tensor.new_empty = boom
+            try:
+                f = fg(shard)
+            finally:
+                for k, v in saved.items():
+                    setattr(torch, k, v)
+                torch.Tensor.new_empty = saved_new
+            if rank == 0:
+                assert f is not None and (not frames or f.data_ptr() == frames[0][0])
+                frames.append((f.data_ptr(), f.numpy().copy()))
+            else:
+                assert f is None
+        if rank == 0:
+            np.save(result_path, np.stack([fr for _, fr in frames]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,H", [(2, 225), (3, 7)])
+def test_frame_gather_allocates_nothing_per_step(tmp_path, world, H):
+    W = 24
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_frame_gather_worker, args=(world, _free_port(), H, W, out), nprocs=world, join=True)
+    frames = np.load(out)
+    for step in range(3):
+        assert np.array_equal(frames[step], _pixel_codes(range(H), W) + step)

@@ -655,17 +655,22 @@ def test_near_tie_culling_is_conservative(gpu_lib, oracle, bvh, competitor):
     competitor is tested first and its hit lies within the slab test's rounding of the small sphere's box
     entry; with the host-padded boxes and the tbest margin the kernel still enters that box, so the frame
     and the segment count are cpu_ref32's (which culls in f64 with a margin) bit for bit, for every BVH
-    builder. The camera lies above the scene's primitive bounds, so the render also widens the margin
-    (ensure_origin_bound); a second camera 100 units up widens it again."""
+    builder. A second camera 2500 units up lies beyond twice the primitives' reach, so its render first
+    widens the margin on the device (ensure_origin_bound; the plan reports the new bound)."""
     from tie_scene import GREEN, colour_counts, near_tie_scene
 
-    for h in (2.0, 100.0):
+    for h in (2.0, 2500.0):
         d, cam = near_tie_scene(bvh, competitor, width=96, cam_height=h)
         ds = gpu_lib.scene_create(d)
+        m0 = ds.plan(cam).origin_bound
         g, st = ds.render_host(cam)
+        m1 = ds.plan(cam).origin_bound
         ds.close()
         o, segs = oracle.render_f32(d, cam)
-        assert colour_counts(o)[GREEN] > 500, h
+        if h < 10:
+            assert colour_counts(o)[GREEN] > 500 and m1 == m0 and 1000 <= m0 <= 1002, (m0, m1)
+        else:
+            assert m0 <= 1002 and m1 >= (1000 + h) / 2, (m0, m1)
         assert np.array_equal(g, o) and st.segments == segs, (h, colour_counts(g), colour_counts(o))
 
 

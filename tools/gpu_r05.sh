@@ -2,6 +2,7 @@
 # tools/gpu_r05.sh OUTDIR STEP... — one GPU-box session (through gpurun, from the repo root). Steps:
 #   tests           pytest -m gpu (failures reported, the session goes on; a crash or timeout ends it)
 #   bench:N         bench.py --config N (BENCH_ARGS appended)
+#   run:NAME:CMD    any command ('+' for spaces), NAME.log
 #   testlib:LIB:EXPR  the GPU tests matching -k EXPR against another build (RTGPU_LIB=LIB); failures
 #                   are the expected outcome of a negative control, so they do not end the session
 #   ab:NAME:ARGS    tools/ab_schedule.py with ARGS (spaces as '+')
@@ -73,6 +74,11 @@ for s in "$@"; do
       args=${rest#*:}
       step "bench_$name" 700 python3 bench.py ${args//+/ } || exit $?
       grep '^{' "$OUT/bench_$name.log" > "$OUT/bench_$name.json" ;;
+    run:*)  # run:NAME:COMMAND — any command ('+' for spaces), output in NAME.log
+      rest=${s#run:}
+      name=${rest%%:*}
+      cmd=${rest#*:}
+      step "$name" 700 ${cmd//+/ } || exit $? ;;
     ab:*)
       rest=${s#ab:}
       name=${rest%%:*}

@@ -501,7 +501,12 @@ enum Geom : int {
   kGeomTreelet = 2,  // nodes below S.treelet_bytes from their LDS copy, the rest through the caches
 };
 
-template <class Stk, bool COUNT, int GEOM>
+// OWN_LEAF (quad-only kernels, identity refs): a ray leaving a quad never hits it again (the origin rule), so
+// the single-quad leaf that holds it is useless; with the conservative culling margin its flat box is thick
+// enough that a ray leaving at a shallow angle enters it (Cornell +6 %, round 5). Its box holds the origin, so
+// its entry key is the floor and it is the nearest child: when the next node is that leaf the lane pops
+// instead. A leaf ~(slot << 3) holds slot alone (a leaf of several quads has count - 1 > 0 in its code).
+template <class Stk, bool COUNT, int GEOM, bool OWN_LEAF = false>
 __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
   constexpr bool PAIRS = GEOM != kGeomLds;
@@ -599,6 +604,9 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
       if (k1 != ~0u) stk.store(t.sp++, code_of(k1));
     }
     t.todo = code_of(k0);
+    if (OWN_LEAF && t.origin >= 0 &&
+        t.todo == ~static_cast<int32_t>((static_cast<uint32_t>(t.origin) & ~static_cast<uint32_t>(kQuadRefBit)) << 3))
+      trav_pop(t, stk);
   }
 }
 
@@ -1336,7 +1344,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       for (int rep = 0; rep < kNodeReps; ++rep) {
         if (at_inner(tr)) {
           if constexpr (WIDE == 4)
-            node_step4<Stk, COUNT, GEOM>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
+            node_step4<Stk, COUNT, GEOM, GEOM == kGeomLds && (PRIMS & kPrimsKind) == kPrimsQuads>(
+                tr, S, stk, w.cnt, w.overflow, w.corrupt);
           else
             node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
         }

@@ -1458,7 +1458,10 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   if (st != RTG_OK) return st;
   if (have_host) rec.swap(s->host_nodes);
   std::vector<int32_t> order;
-  hot_order_nodes(rec.data(), width, cnt.data(), n, &order);
+  if (!hot_order_nodes(rec.data(), width, cnt.data(), n, &order)) {
+    s->host_nodes.clear();  // rec may be the host copy: it no longer claims to match the device array
+    return fail(RTG_E_INVALID, "hot treelet: a BVH inner code outside the node array (corrupt tree)");
+  }
   void* stage = nullptr;  // the renumbered array through pinned memory (one DMA), else from the vector
   if (hipHostMalloc(&stage, n * nb, hipHostMallocDefault) == hipSuccess) {
     std::memcpy(stage, rec.data(), n * nb);
@@ -1589,7 +1592,7 @@ rtg_status rtg_hot_treelet_order_host(int32_t* nodes, const uint32_t* visits, in
         return fail(RTG_E_INVALID, "inner child code outside the node array");
     }
   std::vector<int32_t> order;
-  hot_order_nodes4(nodes, visits, num_nodes, &order);
+  if (!hot_order_nodes4(nodes, visits, num_nodes, &order)) return fail(RTG_E_INVALID, "corrupt node array");
   return RTG_OK;
 }
 
@@ -1611,6 +1614,10 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     P = Plan{};
     pst = plan_render(s, cam, job, &P);
     if (pst != RTG_OK) return pst;
+  } else if (K.verbose && P.variant == 5 && !P.count && s->treelet_key != 0 && treelet_key(cam, job) != s->treelet_key) {
+    // a moved camera keeps the first camera's hot treelet until rtg_scene_prepare re-tunes it
+    std::fprintf(stderr, "[rtg] treelet render with the node order tuned for another camera or shard "
+                         "(rtg_scene_prepare re-tunes it; plan.treelet_hot = 0)\n");
   }
   const int W = P.W, rows = P.rows;
   DevJob& dj = P.dj;

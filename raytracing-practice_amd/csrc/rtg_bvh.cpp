@@ -843,11 +843,18 @@ void reorder_top_bfs(BvhW<W>* t, int64_t top) {
 }
 template void reorder_top_bfs<4>(BvhW<4>*, int64_t);
 
-void hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
+bool hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
   const int64_t words = 7 * width, bytes = 28 * width;  // a node: 6 plane rows + 1 code row of `width`
   std::vector<int32_t>& order = *order_out;
   order.resize(n);
-  if (n <= 1) return;
+  // every inner code must name a node of the array (the array may come from the device builder): a bad
+  // one would index pos[] out of bounds below, so nothing is renumbered
+  for (int64_t k = 0; k < n; ++k)
+    for (int c = 0; c < width; ++c) {
+      const int32_t code = rec[k * words + 6 * width + c];
+      if (code >= 0 && (code % bytes != 0 || code / bytes >= n)) return false;
+    }
+  if (n <= 1) return true;
   for (int64_t k = 0; k < n; ++k) order[k] = static_cast<int32_t>(k);
   // the root stays node 0 (DevScene::root_code); the others by visits, ties in their previous order
   std::stable_sort(order.begin() + 1, order.end(),
@@ -862,6 +869,7 @@ void hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n,
       if (code[c] >= 0) code[c] = static_cast<int32_t>(pos[code[c] / bytes] * bytes);  // inner: byte offset
   }
   std::memcpy(rec, out.data(), static_cast<size_t>(n) * bytes);
+  return true;
 }
 
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {

@@ -109,10 +109,11 @@ void reorder_top_bfs(BvhW<W>* t, int64_t top);
 // Hot treelet (rtg_scene_prepare): renumber n device-format W-wide nodes (28 W bytes = 7 W int32 each:
 // six plane rows, then the code row; inner child = byte offset of its node) so the root stays first
 // and the others follow by descending visits (stable); inner codes remapped, leaf and empty codes
-// unchanged. order_out[k] = the old index of new node k.
-void hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out);
-inline void hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
-  hot_order_nodes(rec, 4, visits, n, order_out);
+// unchanged. order_out[k] = the old index of new node k. Returns false, renumbering nothing, when an inner
+// code does not name a node of the array.
+bool hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out);
+inline bool hot_order_nodes4(int32_t* rec, const uint32_t* visits, int64_t n, std::vector<int32_t>* order_out) {
+  return hot_order_nodes(rec, 4, visits, n, order_out);
 }
 // Device bytes of one node of a W-wide tree (W = 4: 112, W = 8: 224).
 constexpr int node_bytes(int width) { return 28 * width; }

@@ -527,7 +527,9 @@ def main():
                          "algorithmic_bytes_per_launch": int(algo_bytes),
                          "per_segment": {"box_tests": round(cst.box_tests / max(cst.segments, 1), 3),
                                          "prim_tests": round(cst.prim_tests / max(cst.segments, 1), 3),
-                                         "hit_frac": round(cst.hits / max(cst.segments, 1), 4)}},
+                                         "hit_frac": round(cst.hits / max(cst.segments, 1), 4),
+                                         # pushes into the global spill area (4-B store + 4-B load each)
+                                         "stack_spills": round(cst.stack_spills / max(cst.segments, 1), 4)}},
             "launch": plan,
             "msamples_per_s": round(samples / wall / 1e6, 3),
             "rays_per_sample": round(total_segs / samples, 4),

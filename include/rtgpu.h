@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 5
+#define RTG_ABI_VERSION 6
 
 typedef int32_t rtg_status;
 #define RTG_OK 0
@@ -221,6 +221,10 @@ typedef struct rtg_render_stats {
    * [13] unit hand-out, [14] camera rays of fresh samples, [15] traversal setup (trav_begin and
    * the scene-spanning occluder test) */
   uint64_t diag[16];
+  /* ABI 6: RTG_RENDER_COUNT only: traversal-stack pushes that went to the global spill area (entries past
+   * the stack's LDS part; deep trees such as config 5's), each a 4-B store and, at the pop, a 4-B load */
+  uint64_t stack_spills;
+  uint64_t reserved_[3];
 } rtg_render_stats;
 
 typedef struct rtg_scene rtg_scene; /* opaque; owns the device copy of the scene */

@@ -51,7 +51,7 @@ constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
 constexpr int64_t kRingAutoBytes = int64_t(4) << 30;  // full-frame partials above this: the tile ring
-constexpr int kNumCounters = 28;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring)
+constexpr int kNumCounters = 28;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring, [26] stack spills)
 // gfx950 allocates a workgroup's LDS in 1280-byte granules (160 KB = 128 of them): measured with the
 // dual launch, whose two workgroups stop sharing a CU exactly when the rounded sizes pass 160 KB
 constexpr int kLdsGranule = 1280;
@@ -1084,6 +1084,7 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
     stats->samples = s->pending_samples;
     stats->kernel_ms = ms;
     for (int k = 0; k < 16; ++k) stats->diag[k] = c[8 + k];
+    stats->stack_spills = c[26];
   }
   // stats stay filled for diagnosis; the frame is not valid in either case
   if (c[4] != 0)

@@ -262,7 +262,8 @@ struct DevJob {
   // [6] persistent kernels' tile counter, [7] workgroups that could not run the 16-bit LDS stack
   // layout (codes past 16 bits: RTG_E_UNSUPPORTED, nothing rendered), [8..23] schedule diagnostics,
   // [24] tile-ring waits that timed out (RTG_E_INTERNAL: frame incomplete), [25] batches that found
-  // their ring slot still owned by an earlier tile (waits; diagnostic)
+  // their ring slot still owned by an earlier tile (waits; diagnostic), [26] COUNT: traversal-stack pushes
+  // into the global spill area
   unsigned long long* counters;
   int32_t leaf_batch;  // default schedules: run a leaf trip once this many lanes wait at a leaf
   int32_t tiles_x;    // 64-pixel tiles per shard row of tiles

@@ -291,6 +291,7 @@ __device__ __forceinline__ bool sphere_wins_tie(const DevScene& S, int32_t slot,
 template <bool COUNT>
 struct Counts {
   uint32_t box = 0, prim = 0;
+  uint32_t spill = 0;  // stack pushes into the global spill area (counters[26])
 };
 
 // Per-lane traversal state of the child-pair BVH (replaces hittable_list::hit -> bvh_node::hit
@@ -351,6 +352,7 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
 template <int N>
 struct LdsStack {
   int32_t* lds;
+  __device__ __forceinline__ bool spills(int32_t) const { return false; }
   __device__ __forceinline__ int32_t capacity() const { return N; }
   __device__ __forceinline__ void store(int32_t sp, int32_t v) const { lds[sp * 64] = v; }
   __device__ __forceinline__ int32_t load(int32_t sp) const { return lds[sp * 64]; }
@@ -363,6 +365,7 @@ struct LdsStack {
 template <int N>
 struct LdsStack16 {
   int16_t* lds;
+  __device__ __forceinline__ bool spills(int32_t) const { return false; }
   __device__ __forceinline__ int32_t capacity() const { return N; }
   __device__ __forceinline__ void store(int32_t sp, int32_t v) const { lds[sp * 64] = static_cast<int16_t>(v); }
   __device__ __forceinline__ int32_t load(int32_t sp) const { return lds[sp * 64]; }
@@ -373,6 +376,7 @@ struct SpillStack {
   int32_t* spill;  // this lane's global area, entries n.. at spill[(sp - n) * 64]
   int32_t n;       // entries kept in LDS (<= N; J.lds_stack, lowered only by tests)
   int32_t cap;     // n + spill depth
+  __device__ __forceinline__ bool spills(int32_t sp) const { return sp >= n; }
   __device__ __forceinline__ int32_t capacity() const { return cap; }
   __device__ __forceinline__ void store(int32_t sp, int32_t v) const {
     if (__builtin_expect(sp < n, 1))
@@ -434,6 +438,7 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, const Stk&
   const bool hr = rn <= rf && ch.y != kEmptyChild;
   if (hl && hr) {
     const bool lfirst = ln <= rn;
+    if (COUNT) cnt.spill += stk.spills(t.sp) ? 1u : 0u;
     if (t.sp < stk.capacity()) {
       stk.store(t.sp, lfirst ? ch.y : ch.x);
       ++t.sp;
@@ -572,6 +577,8 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
       return;
     }
     const int npush = (k1 != ~0u) + (k2 != ~0u) + (k3 != ~0u);
+    if (COUNT)
+      for (int j = 0; j < npush; ++j) cnt.spill += stk.spills(t.sp + j) ? 1u : 0u;
     if (t.sp + npush > stk.capacity()) {
       overflow = true;
     } else {
@@ -596,6 +603,8 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
     // the host sizes every stack from the tree's structural bound (sum of siblings along a path,
     // Bvh4::max_pushes), so pushes cannot overflow; the check runs in the COUNT diagnostics only
     const int npush = (k1 != ~0u) + (k2 != ~0u) + (k3 != ~0u);
+    if (COUNT)
+      for (int j = 0; j < npush; ++j) cnt.spill += stk.spills(t.sp + j) ? 1u : 0u;
     if (COUNT && t.sp + npush > stk.capacity()) {
       overflow = true;
     } else {
@@ -981,10 +990,12 @@ __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w
     const uint32_t wbox = wave_sum(w.cnt.box);
     const uint32_t wprim = wave_sum(w.cnt.prim);
     const uint32_t whits = wave_sum(w.hits);
+    const uint32_t wspill = wave_sum(w.cnt.spill);
     if (lane == 0) {
       atomicAdd(&J.counters[1], static_cast<unsigned long long>(wbox));
       atomicAdd(&J.counters[2], static_cast<unsigned long long>(wprim));
       atomicAdd(&J.counters[3], static_cast<unsigned long long>(whits));
+      atomicAdd(&J.counters[26], static_cast<unsigned long long>(wspill));
       for (int k = 0; k < 16; ++k) atomicAdd(&J.counters[8 + k], static_cast<unsigned long long>(w.diag[k]));
     }
   }

@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 
-RTG_ABI_VERSION = 5
+RTG_ABI_VERSION = 6
 RTG_OK = 0
 RTG_E_INVALID, RTG_E_HIP, RTG_E_NODEVICE, RTG_E_NOMEM, RTG_E_UNSUPPORTED = -1, -2, -3, -4, -5
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
@@ -101,7 +101,7 @@ class rtg_render_desc(C.Structure):
 class rtg_render_stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("box_tests", C.c_uint64),
                 ("prim_tests", C.c_uint64), ("hits", C.c_uint64), ("kernel_ms", C.c_double),
-                ("diag", C.c_uint64 * 16)]
+                ("diag", C.c_uint64 * 16), ("stack_spills", C.c_uint64), ("reserved_", C.c_uint64 * 3)]
 
 
 class rtg_scene_info(C.Structure):

@@ -117,7 +117,8 @@ def main():
                                                             out.data_ptr(), rtgpu.C.byref(cst)))
                     for k2 in envs[v]:
                         os.environ.pop(k2, None)
-                    counts[v] = (cst.box_tests / max(cst.segments, 1), cst.prim_tests / max(cst.segments, 1))
+                    counts[v] = (cst.box_tests / max(cst.segments, 1), cst.prim_tests / max(cst.segments, 1),
+                                 getattr(cst, "stack_spills", 0) / max(cst.segments, 1))
     base = frames[variants[0]]
     res = {}
     for v in variants:
@@ -130,6 +131,7 @@ def main():
         if v in counts:
             res[key]["box_tests_per_segment"] = round(counts[v][0], 3)
             res[key]["prim_tests_per_segment"] = round(counts[v][1], 3)
+            res[key]["stack_spills_per_segment"] = round(counts[v][2], 4)
     for ds in scenes.values():
         ds.close()
     print(json.dumps({"scene": a.scene, "grid": a.grid, "spp": a.spp, "width": a.width, "depth": a.depth,

@@ -351,7 +351,6 @@ __device__ __forceinline__ void trav_begin(Trav& t, const DevScene& S, V3 o, V3 
 // so the LDS part stays small enough for full occupancy and no tree is too deep.
 template <int N>
 struct LdsStack {
-  static constexpr bool kKey16 = false;
   int32_t* lds;
   __device__ __forceinline__ bool spills(int32_t) const { return false; }
   __device__ __forceinline__ int32_t capacity() const { return N; }
@@ -365,8 +364,6 @@ struct LdsStack {
 // lets a second persistent launch share the CU with book-1 (DESIGN.md §3 "occupancy").
 template <int N>
 struct LdsStack16 {
-  // node codes fit 16 bits: the LDS schedule's node step carries them in its sort keys (node_step4)
-  static constexpr bool kKey16 = true;
   int16_t* lds;
   __device__ __forceinline__ bool spills(int32_t) const { return false; }
   __device__ __forceinline__ int32_t capacity() const { return N; }
@@ -375,7 +372,6 @@ struct LdsStack16 {
 };
 template <int N>
 struct SpillStack {
-  static constexpr bool kKey16 = false;
   int32_t* lds;
   int32_t* spill;  // this lane's global area, entries n.. at spill[(sp - n) * 64]
   int32_t n;       // entries kept in LDS (<= N; J.lds_stack, lowered only by tests)
@@ -479,17 +475,6 @@ __device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, f
   return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
 
-// KEY16 (the LDS schedule with 16-bit stacks): the child's 16-bit code replaces the low half of its entry
-// distance, so the sorted keys carry the codes (no code reads after the sort, one LDS round trip less per
-// node step) and the ordering keeps the distance's top 16 bits (sign, exponent, 7 mantissa bits: children
-// closer than 0.8 % in entry distance may go in either order, which changes the work, never the hit)
-__device__ __forceinline__ uint32_t child_key16(float tnx, float tny, float tnz, float tfx, float tfy,
-                                                float tfz, float tc, uint32_t code16) {
-  const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kCullTMin);
-  const float tf = fminf(fminf(fminf(tfx, tfy), tfz), tc);
-  return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & 0xffff0000u) | code16) : ~0u;
-}
-
 __device__ __forceinline__ void psort(uint32_t& ka, int32_t& ca, uint32_t& kb, int32_t& cb) {
   const bool sw = kb < ka;
   const uint32_t k = sw ? kb : ka;
@@ -530,7 +515,6 @@ template <class Stk, bool COUNT, int GEOM, bool OWN_LEAF = false>
 __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
   constexpr bool PAIRS = GEOM != kGeomLds;
-  constexpr bool KEY16 = GEOM == kGeomLds && Stk::kKey16;
   // 4-wide inner-node codes are byte offsets into the node array (node index * 112)
   // corrupt codes: checked wherever a bad code could fault (nodes through the vector-memory path)
   // and in the COUNT diagnostics; an LDS read outside the allocation cannot fault, and the host
@@ -550,10 +534,6 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   if constexpr (GEOM == kGeomLds) {
     nx = lds_ld4(na + sx), ny = lds_ld4(na + 16 + sy), nz = lds_ld4(na + 32 + sz);
     fx = lds_ld4(na + 48 - sx), fy = lds_ld4(na + 64 - sy), fz = lds_ld4(na + 80 - sz);
-    if constexpr (KEY16) {  // the code row (16-bit codes, masked when the workgroup copied the tree)
-      const nf4 c4 = lds_ld4(na + 96);
-      cc = *reinterpret_cast<const int4*>(&c4);
-    }
   } else {
     if (GEOM == kGeomTreelet && t.todo < S.treelet_bytes) {  // the top of the tree: a ds_read
       const uint32_t la = S.treelet_lds + na;
@@ -578,36 +558,6 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   const f2 fy01 = pk_fma(f2{fy.x, fy.y}, iy, oy), fy23 = pk_fma(f2{fy.z, fy.w}, iy, oy);
   const f2 fz01 = pk_fma(f2{fz.x, fz.y}, iz, oz), fz23 = pk_fma(f2{fz.z, fz.w}, iz, oz);
   const float tc = cull_bound(t.tbest);
-  if constexpr (KEY16) {
-    uint32_t k0 = child_key16(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tc, static_cast<uint32_t>(cc.x));
-    uint32_t k1 = child_key16(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tc, static_cast<uint32_t>(cc.y));
-    uint32_t k2 = child_key16(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tc, static_cast<uint32_t>(cc.z));
-    uint32_t k3 = child_key16(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tc, static_cast<uint32_t>(cc.w));
-    usort(k0, k1);
-    usort(k2, k3);
-    usort(k0, k2);
-    usort(k1, k3);
-    usort(k1, k2);
-    if (k0 == ~0u) {
-      trav_pop(t, stk);
-      return;
-    }
-    const int npush = (k1 != ~0u) + (k2 != ~0u) + (k3 != ~0u);
-    if (COUNT)
-      for (int j = 0; j < npush; ++j) cnt.spill += stk.spills(t.sp + j) ? 1u : 0u;
-    if (COUNT && t.sp + npush > stk.capacity()) {
-      overflow = true;
-    } else {  // a 16-bit stack entry stores the key's low half: the code
-      if (k3 != ~0u) stk.store(t.sp++, static_cast<int32_t>(k3));
-      if (k2 != ~0u) stk.store(t.sp++, static_cast<int32_t>(k2));
-      if (k1 != ~0u) stk.store(t.sp++, static_cast<int32_t>(k1));
-    }
-    t.todo = static_cast<int16_t>(k0 & 0xffffu);
-    if (OWN_LEAF && t.origin >= 0 &&
-        t.todo == ~static_cast<int32_t>((static_cast<uint32_t>(t.origin) & ~static_cast<uint32_t>(kQuadRefBit)) << 3))
-      trav_pop(t, stk);
-    return;
-  }
   uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tc, 0);
   uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tc, 4);
   uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tc, 8);
@@ -1526,12 +1476,6 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
       c.y = c.y >= 0 ? c.y + node_rebase : c.y;
       c.z = c.z >= 0 ? c.z + node_rebase : c.z;
       c.w = c.w >= 0 ? c.w + node_rebase : c.w;
-      if (STK16) {  // 16-bit codes (node_step4 KEY16 puts them in the low half of its sort keys)
-        c.x &= 0xffff;
-        c.y &= 0xffff;
-        c.z &= 0xffff;
-        c.w &= 0xffff;
-      }
       v = *reinterpret_cast<float4*>(&c);
     }
     l_nodes[k] = v;

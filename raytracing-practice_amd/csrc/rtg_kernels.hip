@@ -223,7 +223,7 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
   // roots in (tmin, tmax]: strictly above tmin (interval::surrounds, sphere.hpp:70); a root equal to tmax
-  // is returned for the exact-t tie rule to decide (sphere_wins_tie; round 5)
+  // is returned for the exact-t tie rule to decide (settle_sphere_ties; round 5)
   if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
   if (tmin < lo && lo <= tmax) return lo;
   if (tmin < hi && hi <= tmax) return hi;
@@ -280,12 +280,6 @@ __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
   if (!(best & kQuadRefBit)) return true;
   return qrank > S.tie_rank[S.num_spheres + (best & ~kQuadRefBit)];
-}
-// A sphere (slot `slot`) whose root equals the closest hit `best` (a primitive ref): it takes the hit only
-// from a sphere later in the list (every schedule; S.tie_rank lives in HBM, read only here).
-__device__ __forceinline__ bool sphere_wins_tie(const DevScene& S, int32_t slot, int32_t best) {
-  if (best < 0 || (best & kQuadRefBit)) return false;
-  return S.tie_rank[slot] < S.tie_rank[best];
 }
 
 template <bool COUNT>
@@ -619,6 +613,27 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
+// The sphere tie rule's cold path (leaf_step): the leaf's spheres re-tested against the final closest hit; one
+// at exactly that t from earlier in the list than the closest hit (a sphere) takes it. Not inlined: its
+// registers are then a call's, not the trip loop's (inlined, its sphere test spilled the book-1 kernel's path
+// state: config 2 +3.7 % against a build without the rule, called +2.1 %; round 5). refs: the leaf's
+// primitive refs (null: identity, spheres only).
+__device__ __attribute__((noinline)) int32_t settle_sphere_ties(
+    const float4* spheres, int32_t sphere_f4, const int32_t* refs, const int32_t* tie_rank, int32_t first,
+    int32_t count, float ox, float oy, float oz, float dx, float dy, float dz, float a, float inv_a, float time,
+    float tbest, int32_t best, int32_t origin) {
+  if (best < 0 || (best & kQuadRefBit)) return best;  // a quad (or nothing) keeps an equal-t hit from a sphere
+  const V3 o = v3(ox, oy, oz), d = v3(dx, dy, dz);
+  for (int k = 0; k < count; ++k) {
+    const int32_t ref = refs ? refs[first + k] : first + k;
+    if (ref & kQuadRefBit) continue;
+    const float4* sp4 = spheres + static_cast<int64_t>(ref) * sphere_f4;
+    const float th = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
+    if (th == tbest && tie_rank[ref] < tie_rank[best]) best = ref;
+  }
+  return best;
+}
+
 // Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
 // LDS schedule outside the COUNT diagnostics, as for node codes).
 template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,
@@ -637,20 +652,16 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
   // Sphere ties (DESIGN.md §4 "tie rule") are settled per leaf, off the hot path: the loop takes only roots
   // strictly below the closest hit and flags a lane whose sphere root equalled it; a flagged lane re-tests the
   // leaf's spheres against the final closest hit and takes an equal root from a sphere earlier in the list
-  // (sphere_wins_tie). The rare branch runs once per leaf, not per sphere test (an inline check per sphere
+  // (settle_sphere_ties). The rare branch runs once per leaf, not per sphere test (an inline check per sphere
   // cost book-1 +2 % and the 1M field +7 % in register allocation, round 5).
   bool tie = false;
-  auto settle_ties = [&](auto ref_of) {
+  auto settle_ties = [&](const int32_t* refs) {
     if (ballot_tie(tie) == 0 || !tie) return;
-    for (int k = 0; k < count; ++k) {
-      const int32_t ref = ref_of(k);
-      if (ref & kQuadRefBit) continue;
-      const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
-      const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
-      if (th == t.tbest && sphere_wins_tie(S, ref, t.best)) {
-        t.best = ref;
-        t.mat = MAT ? ibits(sp4[1].w) : -1;
-      }
+    const int32_t nb = settle_sphere_ties(S.spheres, S.sphere_f4, refs, S.tie_rank, first, count, o.x, o.y, o.z, d.x,
+                                          d.y, d.z, t.a, t.inv_a, time, t.tbest, t.best, t.origin);
+    if (nb != t.best) {
+      t.best = nb;
+      t.mat = MAT ? ibits(S.spheres[static_cast<int64_t>(nb) * S.sphere_f4 + 1].w) : -1;
     }
   };
   if ((PRIMS & kPrimsKind) == kPrimsSpheres || ((PRIMS & kPrimsKind) == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
@@ -665,7 +676,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
         t.mat = MAT ? ibits(sp4[1].w) : -1;
       }
     }
-    settle_ties([&](int k) { return first + k; });
+    settle_ties(nullptr);
     pop();
     return;
   }
@@ -701,7 +712,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     }
   }
   if constexpr ((PRIMS & kPrimsKind) != kPrimsQuads)
-    settle_ties([&](int k) { return S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit); });
+    settle_ties(S.ref_mode == 0 ? S.refs : nullptr);
   pop();
 }
 

@@ -222,11 +222,12 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
-  // roots in (tmin, tmax]: strictly above tmin (interval::surrounds, sphere.hpp:70); a root equal to tmax
-  // is returned for the exact-t tie rule to decide (settle_sphere_ties; round 5)
-  if (origin) return (hb < 0.0f && tmin < hi && hi <= tmax) ? hi : -1.0f;
-  if (tmin < lo && lo <= tmax) return lo;
-  if (tmin < hi && hi <= tmax) return hi;
+  // roots strictly inside (tmin, tmax), interval::surrounds (sphere.hpp:70): a sphere never replaces an
+  // equal-t hit; two spheres at the bit-identical t keep the one tested first (DESIGN.md §4 "tie rule": the
+  // list-order form for spheres was measured and rejected in round 5, tools/experiments/sphere_tie_rule.patch)
+  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
+  if (tmin < lo && lo < tmax) return lo;
+  if (tmin < hi && hi < tmax) return hi;
   return -1.0f;
 }
 
@@ -269,11 +270,13 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // closest_so_far (interval::contains, quad.hpp:62, interval.hpp:29), sphere::hit does not
 // (interval::surrounds, sphere.hpp:70, interval.hpp:32). So among the primitives at the smallest t it
 // keeps the last quad of the list if there is one, else the first sphere, whatever order they are tested
-// in. The kernels test in BVH order: sphere_t and quad_t return roots up to tmax; a quad root equal to the
-// closest hit replaces it only if that hit is a sphere or an earlier quad of the list, a sphere root equal
-// to it only if that hit is a later sphere (round 5: duplicate spheres, a ray through a tangent point).
-// S.tie_rank holds each sphere / quad slot's list index and is read only on a tie: the check is one
-// compare and a wave-uniform branch that is almost never taken.
+// in. The kernels test in BVH order: sphere_t returns roots strictly below tmax (a sphere never replaces an
+// equal-t hit), quad_t roots up to tmax, and a quad root equal to the closest hit replaces it only if that
+// hit is a sphere or an earlier quad of the list (S.tie_rank: each quad slot's list index, read only on a
+// tie; the check is one compare and a wave-uniform branch). Two spheres at the bit-identical t keep the one
+// tested first: the one order-dependent case. Its list-order form (round 5) cost config 2 +3.5 %, config 3
+// +8.5 %, config 5 +1.1 % in register allocation for the 14 pixels of 10 M it decides at full spp in
+// configs 2 and 5 (tools/experiments/sphere_tie_rule.patch).
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
@@ -613,27 +616,6 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
-// The sphere tie rule's cold path (leaf_step): the leaf's spheres re-tested against the final closest hit; one
-// at exactly that t from earlier in the list than the closest hit (a sphere) takes it. Not inlined: its
-// registers are then a call's, not the trip loop's (inlined, its sphere test spilled the book-1 kernel's path
-// state: config 2 +3.7 % against a build without the rule, called +2.1 %; round 5). refs: the leaf's
-// primitive refs (null: identity, spheres only).
-__device__ __attribute__((noinline)) int32_t settle_sphere_ties(
-    const float4* spheres, int32_t sphere_f4, const int32_t* refs, const int32_t* tie_rank, int32_t first,
-    int32_t count, float ox, float oy, float oz, float dx, float dy, float dz, float a, float inv_a, float time,
-    float tbest, int32_t best, int32_t origin) {
-  if (best < 0 || (best & kQuadRefBit)) return best;  // a quad (or nothing) keeps an equal-t hit from a sphere
-  const V3 o = v3(ox, oy, oz), d = v3(dx, dy, dz);
-  for (int k = 0; k < count; ++k) {
-    const int32_t ref = refs ? refs[first + k] : first + k;
-    if (ref & kQuadRefBit) continue;
-    const float4* sp4 = spheres + static_cast<int64_t>(ref) * sphere_f4;
-    const float th = sphere_t(sp4[0], sp4[1], o, d, a, inv_a, time, kTMin, tbest, ref == origin);
-    if (th == tbest && tie_rank[ref] < tie_rank[best]) best = ref;
-  }
-  return best;
-}
-
 // Test the primitives of one leaf (t.todo < 0), then pop. CHECK: validate the leaf code (off in the
 // LDS schedule outside the COUNT diagnostics, as for node codes).
 template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,
@@ -649,34 +631,17 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     t.todo = kTravDone;
     return;
   }
-  // Sphere ties (DESIGN.md §4 "tie rule") are settled per leaf, off the hot path: the loop takes only roots
-  // strictly below the closest hit and flags a lane whose sphere root equalled it; a flagged lane re-tests the
-  // leaf's spheres against the final closest hit and takes an equal root from a sphere earlier in the list
-  // (settle_sphere_ties). The rare branch runs once per leaf, not per sphere test (an inline check per sphere
-  // cost book-1 +2 % and the 1M field +7 % in register allocation, round 5).
-  bool tie = false;
-  auto settle_ties = [&](const int32_t* refs) {
-    if (ballot_tie(tie) == 0 || !tie) return;
-    const int32_t nb = settle_sphere_ties(S.spheres, S.sphere_f4, refs, S.tie_rank, first, count, o.x, o.y, o.z, d.x,
-                                          d.y, d.z, t.a, t.inv_a, time, t.tbest, t.best, t.origin);
-    if (nb != t.best) {
-      t.best = nb;
-      t.mat = MAT ? ibits(S.spheres[static_cast<int64_t>(nb) * S.sphere_f4 + 1].w) : -1;
-    }
-  };
   if ((PRIMS & kPrimsKind) == kPrimsSpheres || ((PRIMS & kPrimsKind) == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
     for (int k = 0; k < count; ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
-      tie = tie || th == t.tbest;
-      if (th > 0.0f && th < t.tbest) {
+      if (th > 0.0f) {  // sphere_t: th < tbest
         t.tbest = th;
         t.best = first + k;
         t.mat = MAT ? ibits(sp4[1].w) : -1;
       }
     }
-    settle_ties(nullptr);
     pop();
     return;
   }
@@ -702,8 +667,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
       th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
-      tie = tie || th == t.tbest;
-      take = th > 0.0f && th < t.tbest;
+      take = th > 0.0f;  // sphere_t: th < tbest
     }
     if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;
@@ -711,8 +675,6 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       t.mat = MAT ? m : qrank;
     }
   }
-  if constexpr ((PRIMS & kPrimsKind) != kPrimsQuads)
-    settle_ties(S.ref_mode == 0 ? S.refs : nullptr);
   pop();
 }
 

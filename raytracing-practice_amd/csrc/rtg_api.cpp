@@ -124,22 +124,6 @@ float round_up(double x) {
   if (static_cast<double>(f) < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
   return f;
 }
-// Culling margin (DESIGN.md §4 "conservative culling"): every BVH box plane the kernels test is moved
-// outward by eta = 2^-21 (|plane| + M) before its fp32 rounding (itself outward), where M is the largest
-// |coordinate| of the primitive boxes (so of every hit point a segment starts from). The kernels' slab test
-// fma(plane, rcp(d), -o rcp(d)) errs by at most 3 2^-24 |plane - o| + 2^-24 |o| <= 2^-22 (|plane| + |o|)
-// in world units along the axis (v_rcp_f32: 1 ulp), i.e. <= eta / 2 for every origin with |o| <= M and
-// <= eta for |o| <= 2M (a camera up to twice the scene's reach; ensure_origin_bound widens the pad for one
-// farther out): a computed entry (exit) distance is never past the unpadded box's true one, so no box that
-// holds a primitive hit is culled by rounding; the rest of eta covers the fp32
-// primitive tests' acceptance error (a point the quad test puts inside an edge).
-float pad_down(double lo, double m) {
-  return std::isfinite(lo) ? round_down(lo - 0x1p-21 * (std::fabs(lo) + m)) : static_cast<float>(lo);
-}
-float pad_up(double hi, double m) {
-  return std::isfinite(hi) ? round_up(hi + 0x1p-21 * (std::fabs(hi) + m)) : static_cast<float>(hi);
-}
-
 float ibits_to_float(int32_t i) {
   float f;
   std::memcpy(&f, &i, 4);
@@ -174,6 +158,100 @@ void host_par_for(int64_t n, F&& fn) {
 int host_threads(int64_t n) {
   const int T = std::min(16, std::max(1, static_cast<int>(std::thread::hardware_concurrency())));
   return n < 65536 ? 1 : T;
+}
+
+// Culling margin (DESIGN.md §4 "conservative culling"). Every BVH box the kernels test is the union of its
+// primitives' culling boxes, each the reference's box with every plane v moved outward by an eta that depends
+// on the primitive and the axis, then rounded outward to fp32. M is the largest |coordinate| of the primitive
+// boxes, so of every hit point a later segment starts from; every origin with |o| <= 2M is covered
+// (ensure_origin_bound widens the device boxes for a camera farther out). The kernels' slab test
+// fma(plane, rcp(d), -o rcp(d)) computes a plane's distance t within 3 2^-24 |t| + 2^-24 |o / d| (v_rcp_f32:
+// 1 ulp; the rounded -o rcp(d); the fma); children are culled against fmaf(tbest, 1 + 2^-19, 2^-19) with the
+// exit floor at 0.0009, and kernels that test quads widen every exit distance by 1 + 2^-20 (kCullWiden).
+// - spheres, every axis: eta = 2^-21 (|v| + M) >= 3 2^-24 |v - o| + 2^-24 |o| for |o| <= 2M: no computed entry
+//   (exit) distance is past the unpadded box's true one; the rest covers the discriminant letting a ray
+//   graze a face.
+// - axis-aligned quads (quad_flat_axis; quad_t's root t_c is then within 2 2^-24 of the true crossing t*,
+//   and the hit point it accepts lies past the edge through Q by at most 2^-24 |p| (the sign of p - Q is
+//   exact) and past the far edge by at most 4 2^-24 |u| + 2^-24 |p|): on the flat axis k eta = 2^-23 (|v| + M)
+//   (1 + 2^-16) >= 2^-24 |o| (1 + 2^-20) + the rounding of Q_k; on an in-plane axis a, with U_a the quad's
+//   extent along it, eta = 2^-24 (6 U_a + 3 |v| + 2M) (1 + 2^-10) >= 4 2^-24 U_a (alpha or beta, and p - Q) +
+//   2^-24 (|Q_a| + U_a) (the record's rounded corners) + 2^-24 |p| (p ~ v) + 2^-24 |o| (|o| <= 2M), so a quad's
+//   box reaches past its neighbours' planes by less than the exit floor for most rays leaving them (Cornell's
+//   blocks: a ray leaving a face enters the block's node when that reach exceeds 0.0009 of its exit
+//   distance). What grows with the distance
+//   (the slab's and quad_t's relative errors, <= 5 2^-24 of t) is taken by kCullWiden, so the computed entry
+//   distance never exceeds the computed exit of a box holding an accepted hit, nor the cull bound. A flat box
+//   stays thin: a ray leaving the quad at a shallow angle leaves it before the exit floor.
+// - other quads, every axis: eta = 2^-18 (|v| + M): their float normal and plane distance are rounded, so
+//   the accepted points leave the corners' box by a few 2^-24 (|v| + M) plus 2^-24 of the distance
+//   (<= |v| + 2M), all taken in the pad.
+// The flat axis of an axis-aligned quad (u and v each along one coordinate axis, so the record's normal is
+// exactly +-e_k, its plane distance +-Q_k, and alpha / beta each depend on one coordinate of the hit point),
+// or -1.
+int quad_flat_axis(const rtg_primitive& p) {
+  auto axis_of = [](const double v[3]) {
+    const int nz = (v[0] != 0.0) + (v[1] != 0.0) + (v[2] != 0.0);
+    return nz != 1 ? -1 : v[0] != 0.0 ? 0 : v[1] != 0.0 ? 1 : 2;
+  };
+  const int i = axis_of(p.p1), j = axis_of(p.p2);
+  if (i < 0 || j < 0 || i == j) return -1;
+  const int k = 3 - i - j;
+  const D3 n = unit_vector(cross(d3(p.p1), d3(p.p2)));  // as the quad record's normal (compile_scene)
+  const double c[3] = {n.x, n.y, n.z};
+  return std::fabs(c[k]) == 1.0 && c[i] == 0.0 && c[j] == 0.0 ? k : -1;
+}
+void culling_box(const rtg_primitive& p, double m, double lo[3], double hi[3]) {
+  prim_bbox(p, lo, hi);
+  const int flat = p.kind == RTG_PRIM_QUAD ? quad_flat_axis(p) : -1;
+  if (flat >= 0) lo[flat] = hi[flat] = p.p0[flat];  // the reference's 0.0001 minimum extent is not needed here
+  for (int a = 0; a < 3; ++a) {
+    if (p.kind == RTG_PRIM_QUAD && flat >= 0 && a != flat) {  // in-plane: 2^-24 (6 |U_a| + 3 |v| + 2M)
+      const double ua = std::fabs(p.p1[a]) + std::fabs(p.p2[a]), k = 0x1p-24 * (1.0 + 0x1p-10);
+      lo[a] -= k * (6.0 * ua + 3.0 * std::fabs(lo[a]) + 2.0 * m);
+      hi[a] += k * (6.0 * ua + 3.0 * std::fabs(hi[a]) + 2.0 * m);
+      continue;
+    }
+    const double c = p.kind == RTG_PRIM_SPHERE ? 0x1p-21 : flat < 0 ? 0x1p-18 : 0x1p-23 * (1.0 + 0x1p-16);
+    lo[a] -= c * (std::fabs(lo[a]) + m);
+    hi[a] += c * (std::fabs(hi[a]) + m);
+  }
+}
+// Replace the child boxes of a built tree (binary or W-wide; leaves -(1 + first ref), count) by the unions of
+// their primitives' culling boxes. The tree itself (built from the reference's boxes) is unchanged.
+template <class Node, int W>
+void refit_culling_boxes(std::vector<Node>& nodes, const std::vector<int64_t>& refs, const rtg_scene_desc* d,
+                         double m) {
+  if (nodes.empty()) return;
+  std::vector<std::array<double, 6>> pb(refs.size());
+  host_par_for(static_cast<int64_t>(refs.size()), [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) culling_box(d->prims[refs[i]], m, pb[i].data(), pb[i].data() + 3);
+  });
+  struct Refit {
+    std::vector<Node>& nodes;
+    const std::vector<std::array<double, 6>>& pb;
+    void node(int32_t k, double lo[3], double hi[3]) {  // refits node k, returns the union of its children
+      Node& n = nodes[k];
+      for (int a = 0; a < 3; ++a) lo[a] = HUGE_VAL, hi[a] = -HUGE_VAL;
+      for (int c = 0; c < W; ++c) {
+        if (n.child[c] == kEmptyChild) continue;
+        double cl[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL}, ch[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+        if (n.child[c] >= 0) {
+          node(n.child[c], cl, ch);
+        } else {
+          const int64_t first = -(static_cast<int64_t>(n.child[c]) + 1);
+          for (int64_t r = first; r < first + n.count[c]; ++r)
+            for (int a = 0; a < 3; ++a) cl[a] = std::min(cl[a], pb[r][a]), ch[a] = std::max(ch[a], pb[r][3 + a]);
+        }
+        for (int a = 0; a < 3; ++a) {
+          n.lo[c][a] = cl[a], n.hi[c][a] = ch[a];
+          lo[a] = std::min(lo[a], cl[a]), hi[a] = std::max(hi[a], ch[a]);
+        }
+      }
+    }
+  } rf{nodes, pb};
+  double lo[3], hi[3];
+  rf.node(0, lo, hi);
 }
 
 bool texture_uses_uv(const rtg_scene_desc* d, int32_t tex, int depth) {
@@ -293,7 +371,6 @@ void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* o) {
 // kEmptyChild with the inverted box (+inf, -inf). Boxes rounded outward to fp32.
 template <int W>
 bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
-  const double M = out->origin_bound;
   constexpr int64_t kBytes = node_bytes(W), kWords = 7 * W;
   if (t.nodes.size() > static_cast<size_t>(INT32_MAX / kBytes)) {
     *err = "BVH too large for 32-bit node offsets";
@@ -326,8 +403,8 @@ bool emit_wide(const BvhW<W>& t, HostScene* out, std::string* err) {
           }
         }
         for (int a = 0; a < 3; ++a) {
-          f[a * W + c] = empty ? std::numeric_limits<float>::infinity() : pad_down(n.lo[c][a], M);
-          f[3 * W + a * W + c] = empty ? -std::numeric_limits<float>::infinity() : pad_up(n.hi[c][a], M);
+          f[a * W + c] = empty ? std::numeric_limits<float>::infinity() : round_down(n.lo[c][a]);
+          f[3 * W + a * W + c] = empty ? -std::numeric_limits<float>::infinity() : round_up(n.hi[c][a]);
         }
         f[6 * W + c] = ibits_to_float(code);
       }
@@ -386,8 +463,8 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       return false;
     }
   }
-  // M of the culling margin (pad_down): the largest |coordinate| of any primitive box, i.e. of any hit
-  // point a later segment starts from; rtg_render widens the pad when a camera lies farther out
+  // M of the culling margin (culling_box): the largest |coordinate| of any primitive box, i.e. of any hit
+  // point a later segment starts from; rtg_render widens the boxes when a camera lies farther out
   {
     const int T = host_threads(d->num_prims);
     std::vector<double> part(T, 0.0);
@@ -579,7 +656,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     if (slot[i] >= 0)
       out->tie_rank[(d->prims[i].kind == RTG_PRIM_QUAD ? nsph : 0) + slot[i]] = static_cast<int32_t>(i);
   phase("prims");
-  // leaf code = ~((first << 3) | (count - 1)); boxes rounded outward
+  // culling boxes (the margin above) in place of the reference's, then rounded outward
+  if (out->node_width == 4) refit_culling_boxes<BuildNode4, 4>(bvh4.nodes, bvh.refs, d, out->origin_bound);
+  if (out->node_width == 2) refit_culling_boxes<BuildNode, 2>(bvh.nodes, bvh.refs, d, out->origin_bound);
+  // leaf code = ~((first << 3) | (count - 1))
   if (out->node_width == 4 && !emit_wide(bvh4, out, err)) return false;
   // child-pair nodes: 64 B
   if (out->node_width == 2) out->nodes.resize(bvh.nodes.size() * 16);
@@ -601,8 +681,8 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         continue;
       }
       for (int a = 0; a < 3; ++a) {
-        lo[s][a] = pad_down(n.lo[s][a], out->origin_bound);
-        hi[s][a] = pad_up(n.hi[s][a], out->origin_bound);
+        lo[s][a] = round_down(n.lo[s][a]);
+        hi[s][a] = round_up(n.hi[s][a]);
       }
       if (n.child[s] >= 0) {
         code[s] = n.child[s];
@@ -953,7 +1033,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scen
     GpuBvhResult r{};
     e = gpu_build_bvh4(reinterpret_cast<const float4*>(base + parts[2].off),
                        reinterpret_cast<const float4*>(base + parts[3].off), refs_dev, nrefs,
-                       round_up(0x1p-21 * hs.origin_bound), reinterpret_cast<float*>(base + parts[0].off),
+                       round_up(hs.origin_bound), reinterpret_cast<float*>(base + parts[0].off),
                        hs.node_capacity, sorted, &r, s->own_stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(refs_dev, sorted, nrefs * 4, hipMemcpyDeviceToDevice, s->own_stream);
@@ -1490,10 +1570,11 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   return RTG_OK;
 }
 
-// The culling margin covers ray origins with |coordinate| <= 2 s->origin_bound (pad_down: M = the primitive
-// boxes' reach when the scene was created). A camera whose lens reaches farther out widens the pad of every
+// The culling margin covers ray origins with |coordinate| <= 2 s->origin_bound (culling_box: M = the
+// primitive boxes' reach when the scene was created). A camera whose lens reaches farther out widens every
 // node box on the device first (repad_nodes_kernel, on the render's stream; 1/16 headroom so a camera moving
-// about does not repad every frame). Boxes only grow: frames are unchanged, the bound holds again.
+// about does not repad every frame) by 2^-20 per unit of M added: the most any margin's origin terms grow (a
+// quad's in-plane axes, 7 2^-24 |o|). Boxes only grow: frames are unchanged, the bound holds again.
 rtg_status ensure_origin_bound(rtg_scene* s, const rtg_camera_desc* cam, hipStream_t stream) {
   if (s->dev.num_nodes <= 0) return RTG_OK;
   rtg_camera_params cp;
@@ -1504,7 +1585,7 @@ rtg_status ensure_origin_bound(rtg_scene* s, const rtg_camera_desc* cam, hipStre
   if (mc <= 2.0 * s->origin_bound) return RTG_OK;
   if (!(mc < 1e30)) return fail(RTG_E_INVALID, "camera position not finite (or above 1e30)");
   const double target = 0.5 * mc * (1.0 + 1.0 / 16.0);
-  const float delta = round_up(0x1p-21 * (target - s->origin_bound));
+  const float delta = round_up(0x1p-20 * (target - s->origin_bound));
   RTG_HIP(launch_repad(reinterpret_cast<float*>(const_cast<float4*>(s->dev.nodes)), s->dev.num_nodes,
                        s->dev.node_width, delta, stream),
           "repad kernel launch");

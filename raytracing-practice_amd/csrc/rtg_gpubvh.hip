@@ -33,20 +33,26 @@ struct Box6 {
   float lo[3], hi[3];
 };
 
-// The culling margin of the host builder (rtg_api.cpp pad_down; DESIGN.md §4 "conservative culling"):
-// planes move outward by 2^-21 (|v| + M) for the slab test's rounding, here 2^-20 |v| + pad_abs
-// (pad_abs >= 2^-21 M, rounded up on the host) so that the box's own fp32 arithmetic (centre +- r, the
-// corner sums, this subtraction: a few 2^-24 |v|) is covered as well
-__device__ __forceinline__ float pad_lo(float v, float pad_abs) { return v - (fabsf(v) * 0x1p-20f + pad_abs); }
-__device__ __forceinline__ float pad_hi(float v, float pad_abs) { return v + (fabsf(v) * 0x1p-20f + pad_abs); }
+// The culling margin of the host builder (rtg_api.cpp culling_box; DESIGN.md §4 "conservative culling"):
+// each plane moves outward by c (|v| + M), c = 2^-21 for spheres, 2^-23 (1 + 2^-16) on an axis-aligned quad's
+// flat axis and 2^-24 (6 U + 3 |v| + 2M) on its in-plane axes (U its extent there), 2^-18 on every axis of
+// other quads; here the M terms come from the host
+// (pads, rounded up) and the |v| terms are doubled, so that the box's own fp32 arithmetic (centre +- r, the
+// corner sums, the minimum extent, this subtraction: a few 2^-24 |v|) is covered as well
+struct CullPads {
+  float sphere, quad, flat, inplane;  // 2^-21 M, 2^-18 M, 2^-23 M (1 + 2^-16), 2^-23 M; rounded up
+};
+__device__ __forceinline__ float pad_by(float v, float rel, float abs_pad) { return fabsf(v) * rel + abs_pad; }
 
-// Box of one primitive record (the fp32 records the render kernels intersect), unpadded; thin axes get
-// the reference's 0.0001 minimum extent (aabb::pad_to_minimums, aabb.hpp:135-154).
-__device__ Box6 prim_box(const float4* spheres, const float4* quads, int32_t ref) {
+// Box of one primitive record (the fp32 records the render kernels intersect), unpadded; thin axes other
+// than an axis-aligned quad's flat one get the reference's 0.0001 minimum extent (aabb::pad_to_minimums,
+// aabb.hpp:135-154).
+__device__ Box6 prim_box(const float4* spheres, const float4* quads, int32_t ref, int* flat) {
   Box6 b;
+  *flat = -1;
   if (ref & kQuadRefBit) {
     const float4* q = quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
-    const float4 Q = q[0], u = q[1], v = q[2];
+    const float4 Q = q[0], u = q[1], v = q[2], n = q[4];
     const float px[4] = {Q.x, Q.x + u.x, Q.x + v.x, Q.x + u.x + v.x};
     const float py[4] = {Q.y, Q.y + u.y, Q.y + v.y, Q.y + u.y + v.y};
     const float pz[4] = {Q.z, Q.z + u.z, Q.z + v.z, Q.z + u.z + v.z};
@@ -56,6 +62,14 @@ __device__ Box6 prim_box(const float4* spheres, const float4* quads, int32_t ref
     b.hi[0] = fmaxf(fmaxf(px[0], px[1]), fmaxf(px[2], px[3]));
     b.hi[1] = fmaxf(fmaxf(py[0], py[1]), fmaxf(py[2], py[3]));
     b.hi[2] = fmaxf(fmaxf(pz[0], pz[1]), fmaxf(pz[2], pz[3]));
+    // flat axis (rtg_api.cpp quad_flat_axis): u and v each along one coordinate axis, normal exactly +-e_k
+    const int nu = (u.x != 0.0f) + (u.y != 0.0f) + (u.z != 0.0f), nv = (v.x != 0.0f) + (v.y != 0.0f) + (v.z != 0.0f);
+    const int iu = u.x != 0.0f ? 0 : u.y != 0.0f ? 1 : 2, iv = v.x != 0.0f ? 0 : v.y != 0.0f ? 1 : 2;
+    if (nu == 1 && nv == 1 && iu != iv) {
+      const int k = 3 - iu - iv;
+      const float nn[3] = {n.x, n.y, n.z};
+      if (fabsf(nn[k]) == 1.0f && nn[iu] == 0.0f && nn[iv] == 0.0f) *flat = k;
+    }
   } else {
     const float4 s0 = spheres[static_cast<int64_t>(ref) * 2];
     const float4 s1 = spheres[static_cast<int64_t>(ref) * 2 + 1];
@@ -68,7 +82,7 @@ __device__ Box6 prim_box(const float4* spheres, const float4* quads, int32_t ref
     }
   }
   for (int k = 0; k < 3; ++k) {
-    if (b.hi[k] - b.lo[k] < 0.0001f) {
+    if (b.hi[k] - b.lo[k] < 0.0001f && k != *flat) {  // a flat axis gets its own pad (prim_bounds_kernel)
       b.lo[k] -= 0.00005f;
       b.hi[k] += 0.00005f;
     }
@@ -86,16 +100,31 @@ __device__ __forceinline__ float o2f(uint32_t u) {
 }
 
 __global__ void prim_bounds_kernel(const float4* spheres, const float4* quads, const int32_t* refs, int64_t n,
-                                   float pad_abs, Box6* boxes, uint32_t* cbounds) {
+                                   CullPads pads, Box6* boxes, uint32_t* cbounds) {
   const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   float c[3] = {0.0f, 0.0f, 0.0f};
   const bool ok = i < n;
   if (ok) {
-    Box6 b = prim_box(spheres, quads, refs[i]);
+    const int32_t ref = refs[i];
+    int flat;
+    Box6 b = prim_box(spheres, quads, ref, &flat);
+    const bool quad = (ref & kQuadRefBit) != 0;
+    float qu[3] = {0.0f, 0.0f, 0.0f}, qv[3] = {0.0f, 0.0f, 0.0f};
+    if (quad) {
+      const float4* q = quads + static_cast<int64_t>(ref & ~kQuadRefBit) * 5;
+      const float4 u = q[1], v = q[2];
+      qu[0] = u.x, qu[1] = u.y, qu[2] = u.z, qv[0] = v.x, qv[1] = v.y, qv[2] = v.z;
+    }
     for (int k = 0; k < 3; ++k) {  // centroid of the unpadded box: Morton codes independent of the margin
       c[k] = 0.5f * (b.lo[k] + b.hi[k]);
-      b.lo[k] = pad_lo(b.lo[k], pad_abs);
-      b.hi[k] = pad_hi(b.hi[k], pad_abs);
+      // in-plane axis of an axis-aligned quad: 2^-24 (6 U_k + 3 |v| + 2M) as on the host, here 8 and 8 2^-24
+      const bool inplane = quad && flat >= 0 && k != flat;
+      const float rel = !quad || inplane ? 0x1p-20f : k == flat ? 0x1p-22f : 0x1p-17f;
+      const float ab = !quad ? pads.sphere
+                       : inplane ? fmaf(fabsf(qu[k]) + fabsf(qv[k]), 0x1p-21f, pads.inplane)
+                       : k == flat ? pads.flat : pads.quad;
+      b.lo[k] -= pad_by(b.lo[k], rel, ab);
+      b.hi[k] += pad_by(b.hi[k], rel, ab);
     }
     boxes[i] = b;
   }
@@ -348,7 +377,7 @@ unsigned blocks_for(int64_t n) { return static_cast<unsigned>((n + 255) / 256); 
 // Builds the 4-wide BVH of n primitive refs (refs_in: input order) on the device. Writes up to
 // max_nodes nodes (28 floats each) to `nodes` and the leaf-ordered refs to `refs_out` (n entries).
 hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int32_t* refs_in, int64_t n,
-                          float pad_abs, float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
+                          float m, float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
                           hipStream_t st) {
   *res = GpuBvhResult{};
   if (n <= 0) return hipSuccess;
@@ -399,8 +428,12 @@ hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int3
   do {
     const uint32_t cb_init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
     if ((err = hipMemcpyAsync(cb, cb_init, sizeof(cb_init), hipMemcpyHostToDevice, st)) != hipSuccess) break;
+    // M terms of the culling pads (m: M rounded up; power-of-two scalings are exact, the flat factor is
+    // rounded up by one ulp)
+    const CullPads pads{m * 0x1p-21f, m * 0x1p-18f, __builtin_nextafterf(m * 0x1p-23f * (1.0f + 0x1p-16f), __builtin_inff()),
+                        m * 0x1p-23f};
     hipLaunchKernelGGL(prim_bounds_kernel, dim3(blocks_for(n)), dim3(256), 0, st, spheres, quads, refs_in, n,
-                       pad_abs, boxes, cb);
+                       pads, boxes, cb);
     hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(n)), dim3(256), 0, st, boxes, n, cb, codes, ids);
     if ((err = rocprim::radix_sort_pairs(P(o_sort), sort_bytes, codes, codes2, ids, ids2, static_cast<size_t>(n), 0,
                                          30, st)) != hipSuccess)

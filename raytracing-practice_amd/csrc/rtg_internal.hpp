@@ -207,9 +207,9 @@ struct GpuBvhResult {  // rtg_gpubvh.hip
   int32_t depth;
   int32_t stack_need;
 };
-// pad_abs: the culling margin's origin term (>= 2^-21 M, HostScene::origin_bound)
+// m: M of the culling margin (HostScene::origin_bound, rounded up; rtg_api.cpp culling_box)
 hipError_t gpu_build_bvh4(const float4* spheres, const float4* quads, const int32_t* refs_in, int64_t n,
-                          float pad_abs, float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
+                          float m, float* nodes, int64_t max_nodes, int32_t* refs_out, GpuBvhResult* res,
                           hipStream_t st);
 
 constexpr int kLdsStack = 16;  // LDS stack entries per lane of the persistent kernel

@@ -42,6 +42,11 @@ constexpr float kCullTMin = 0.0009f;
 constexpr float kCullRel = 1.0f + 0x1p-19f;
 constexpr float kCullAbs = 0x1p-19f;
 __device__ __forceinline__ float cull_bound(float tbest) { return fmaf(tbest, kCullRel, kCullAbs); }
+// Exit distances of a child box are multiplied by kCullWiden before the entry <= exit compare in kernels
+// that test quads: the slab test's relative error (3 2^-24 of t per plane) and quad_t's (2 2^-24) are then
+// taken in t, and the boxes need padding only for the errors that do not grow with the distance (rtg_api.cpp
+// culling_box). Sphere-only kernels keep the plain compare (their boxes carry the distance terms).
+constexpr float kCullWiden = 1.0f + 0x1p-20f;
 constexpr float kPi = 3.14159265358979323846f;
 constexpr int kMaxTexNesting = 16;
 
@@ -425,9 +430,9 @@ __device__ __forceinline__ void node_step(Trav& t, const DevScene& S, const Stk&
   const float r0z = fmaf(c.x, inv.z, oi.z), r1z = fmaf(c.w, inv.z, oi.z);
   const float tc = cull_bound(t.tbest);
   const float ln = fmaxf(fmaxf(fminf(l0x, l1x), fminf(l0y, l1y)), fmaxf(fminf(l0z, l1z), kCullTMin));
-  const float lf = fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fminf(fmaxf(l0z, l1z), tc));
+  const float lf = fminf(fminf(fminf(fmaxf(l0x, l1x), fmaxf(l0y, l1y)), fmaxf(l0z, l1z)) * kCullWiden, tc);
   const float rn = fmaxf(fmaxf(fminf(r0x, r1x), fminf(r0y, r1y)), fmaxf(fminf(r0z, r1z), kCullTMin));
-  const float rf = fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fminf(fmaxf(r0z, r1z), tc));
+  const float rf = fminf(fminf(fminf(fmaxf(r0x, r1x), fmaxf(r0y, r1y)), fmaxf(r0z, r1z)) * kCullWiden, tc);
   // An empty slot (right child only; the host guarantees the left one is never empty) has an
   // inverted box, which the symmetric min/max slab form would report as all of space: test
   // the child code explicitly.
@@ -463,13 +468,12 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 
 // Entry distance of one child (tn) or a miss: the slab test with the near/far planes already
 // chosen by the ray's direction signs, so no min/max between a slab's two planes is needed.
+// tf: the child's exit distance (min over the far planes, widened by kCullWiden in quad kernels);
 // tc: the cull bound of the closest hit so far (cull_bound)
-__device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, float tfx, float tfy,
-                                              float tfz, float tc, uint32_t slot) {
+__device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, float tf, float tc, uint32_t slot) {
   const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kCullTMin);
-  const float tf = fminf(fminf(fminf(tfx, tfy), tfz), tc);
   // tn >= kCullTMin > 0, so its bits order like the float; the low 4 bits carry the slot (x4)
-  return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
+  return tn <= fminf(tf, tc) ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
 
 __device__ __forceinline__ void psort(uint32_t& ka, int32_t& ca, uint32_t& kb, int32_t& cb) {
@@ -503,12 +507,8 @@ enum Geom : int {
   kGeomTreelet = 2,  // nodes below S.treelet_bytes from their LDS copy, the rest through the caches
 };
 
-// OWN_LEAF (quad-only kernels, identity refs): a ray leaving a quad never hits it again (the origin rule), so
-// the single-quad leaf that holds it is useless; with the conservative culling margin its flat box is thick
-// enough that a ray leaving at a shallow angle enters it (Cornell +6 %, round 5). Its box holds the origin, so
-// its entry key is the floor and it is the nearest child: when the next node is that leaf the lane pops
-// instead. A leaf ~(slot << 3) holds slot alone (a leaf of several quads has count - 1 > 0 in its code).
-template <class Stk, bool COUNT, int GEOM, bool OWN_LEAF = false>
+// WIDEN (kernels that test quads): exit distances widened by kCullWiden (DESIGN.md §4 "conservative culling").
+template <class Stk, bool COUNT, int GEOM, bool WIDEN = true>
 __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk& stk, Counts<COUNT>& cnt,
                                            bool& overflow, bool& corrupt) {
   constexpr bool PAIRS = GEOM != kGeomLds;
@@ -555,10 +555,16 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   const f2 fy01 = pk_fma(f2{fy.x, fy.y}, iy, oy), fy23 = pk_fma(f2{fy.z, fy.w}, iy, oy);
   const f2 fz01 = pk_fma(f2{fz.x, fz.y}, iz, oz), fz23 = pk_fma(f2{fz.z, fz.w}, iz, oz);
   const float tc = cull_bound(t.tbest);
-  uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tc, 0);
-  uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tc, 4);
-  uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tc, 8);
-  uint32_t k3 = child_key(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tc, 12);
+  f2 tf01 = {fminf(fminf(fx01.x, fy01.x), fz01.x), fminf(fminf(fx01.y, fy01.y), fz01.y)};
+  f2 tf23 = {fminf(fminf(fx23.x, fy23.x), fz23.x), fminf(fminf(fx23.y, fy23.y), fz23.y)};
+  if constexpr (WIDEN) {  // one v_pk_mul_f32 per child pair
+    tf01 = tf01 * f2{kCullWiden, kCullWiden};
+    tf23 = tf23 * f2{kCullWiden, kCullWiden};
+  }
+  uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, tf01.x, tc, 0);
+  uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, tf01.y, tc, 4);
+  uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, tf23.x, tc, 8);
+  uint32_t k3 = child_key(nx23.y, ny23.y, nz23.y, tf23.y, tc, 12);
   if constexpr (PAIRS) {
     // scene in global memory: the codes travel with their keys through the network, so no second
     // memory round trip sits between the sort and the next node load (-3.6 % on config 5; with
@@ -610,9 +616,6 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
       if (k1 != ~0u) stk.store(t.sp++, code_of(k1));
     }
     t.todo = code_of(k0);
-    if (OWN_LEAF && t.origin >= 0 &&
-        t.todo == ~static_cast<int32_t>((static_cast<uint32_t>(t.origin) & ~static_cast<uint32_t>(kQuadRefBit)) << 3))
-      trav_pop(t, stk);
   }
 }
 
@@ -1328,8 +1331,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       for (int rep = 0; rep < kNodeReps; ++rep) {
         if (at_inner(tr)) {
           if constexpr (WIDE == 4)
-            node_step4<Stk, COUNT, GEOM, GEOM == kGeomLds && (PRIMS & kPrimsKind) == kPrimsQuads>(
-                tr, S, stk, w.cnt, w.overflow, w.corrupt);
+            node_step4<Stk, COUNT, GEOM, (PRIMS & kPrimsKind) != kPrimsSpheres>(tr, S, stk, w.cnt, w.overflow,
+                                                                                w.corrupt);
           else
             node_step<Stk, COUNT>(tr, S, stk, w.cnt, w.overflow, w.corrupt);
         }

@@ -468,11 +468,18 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 
 // Entry distance of one child (tn) or a miss: the slab test with the near/far planes already
 // chosen by the ray's direction signs, so no min/max between a slab's two planes is needed.
-// tf: the child's exit distance (min over the far planes, widened by kCullWiden in quad kernels);
 // tc: the cull bound of the closest hit so far (cull_bound)
-__device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, float tf, float tc, uint32_t slot) {
+__device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, float tfx, float tfy, float tfz,
+                                              float tc, uint32_t slot) {
   const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kCullTMin);
+  const float tf = fminf(fminf(fminf(tfx, tfy), tfz), tc);
   // tn >= kCullTMin > 0, so its bits order like the float; the low 4 bits carry the slot (x4)
+  return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
+}
+// the same with the exit distance tf already formed (the far planes' minimum times kCullWiden: quad kernels)
+__device__ __forceinline__ uint32_t child_key_exit(float tnx, float tny, float tnz, float tf, float tc,
+                                                   uint32_t slot) {
+  const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kCullTMin);
   return tn <= fminf(tf, tc) ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
 
@@ -555,16 +562,22 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   const f2 fy01 = pk_fma(f2{fy.x, fy.y}, iy, oy), fy23 = pk_fma(f2{fy.z, fy.w}, iy, oy);
   const f2 fz01 = pk_fma(f2{fz.x, fz.y}, iz, oz), fz23 = pk_fma(f2{fz.z, fz.w}, iz, oz);
   const float tc = cull_bound(t.tbest);
-  f2 tf01 = {fminf(fminf(fx01.x, fy01.x), fz01.x), fminf(fminf(fx01.y, fy01.y), fz01.y)};
-  f2 tf23 = {fminf(fminf(fx23.x, fy23.x), fz23.x), fminf(fminf(fx23.y, fy23.y), fz23.y)};
+  uint32_t k0, k1, k2, k3;
   if constexpr (WIDEN) {  // one v_pk_mul_f32 per child pair
-    tf01 = tf01 * f2{kCullWiden, kCullWiden};
-    tf23 = tf23 * f2{kCullWiden, kCullWiden};
+    const f2 tf01 = f2{fminf(fminf(fx01.x, fy01.x), fz01.x), fminf(fminf(fx01.y, fy01.y), fz01.y)} *
+                    f2{kCullWiden, kCullWiden};
+    const f2 tf23 = f2{fminf(fminf(fx23.x, fy23.x), fz23.x), fminf(fminf(fx23.y, fy23.y), fz23.y)} *
+                    f2{kCullWiden, kCullWiden};
+    k0 = child_key_exit(nx01.x, ny01.x, nz01.x, tf01.x, tc, 0);
+    k1 = child_key_exit(nx01.y, ny01.y, nz01.y, tf01.y, tc, 4);
+    k2 = child_key_exit(nx23.x, ny23.x, nz23.x, tf23.x, tc, 8);
+    k3 = child_key_exit(nx23.y, ny23.y, nz23.y, tf23.y, tc, 12);
+  } else {
+    k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tc, 0);
+    k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tc, 4);
+    k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tc, 8);
+    k3 = child_key(nx23.y, ny23.y, nz23.y, fx23.y, fy23.y, fz23.y, tc, 12);
   }
-  uint32_t k0 = child_key(nx01.x, ny01.x, nz01.x, tf01.x, tc, 0);
-  uint32_t k1 = child_key(nx01.y, ny01.y, nz01.y, tf01.y, tc, 4);
-  uint32_t k2 = child_key(nx23.x, ny23.x, nz23.x, tf23.x, tc, 8);
-  uint32_t k3 = child_key(nx23.y, ny23.y, nz23.y, tf23.y, tc, 12);
   if constexpr (PAIRS) {
     // scene in global memory: the codes travel with their keys through the network, so no second
     // memory round trip sits between the sort and the next node load (-3.6 % on config 5; with

@@ -167,7 +167,8 @@ int host_threads(int64_t n) {
 // (ensure_origin_bound widens the device boxes for a camera farther out). The kernels' slab test
 // fma(plane, rcp(d), -o rcp(d)) computes a plane's distance t within 3 2^-24 |t| + 2^-24 |o / d| (v_rcp_f32:
 // 1 ulp; the rounded -o rcp(d); the fma); children are culled against fmaf(tbest, 1 + 2^-19, 2^-19) with the
-// exit floor at 0.0009, and kernels that test quads widen every exit distance by 1 + 2^-20 (kCullWiden).
+// exit floor at 0.0009, and kernels that test quads compare the entry with min(exit, tbest) (1 + 2^-19)
+// instead (kCullWiden: the relative margin taken on the exit distance too).
 // - spheres, every axis: eta = 2^-21 (|v| + M) >= 3 2^-24 |v - o| + 2^-24 |o| for |o| <= 2M: no computed entry
 //   (exit) distance is past the unpadded box's true one; the rest covers the discriminant letting a ray
 //   graze a face.

@@ -42,11 +42,13 @@ constexpr float kCullTMin = 0.0009f;
 constexpr float kCullRel = 1.0f + 0x1p-19f;
 constexpr float kCullAbs = 0x1p-19f;
 __device__ __forceinline__ float cull_bound(float tbest) { return fmaf(tbest, kCullRel, kCullAbs); }
-// Exit distances of a child box are multiplied by kCullWiden before the entry <= exit compare in kernels
-// that test quads: the slab test's relative error (3 2^-24 of t per plane) and quad_t's (2 2^-24) are then
-// taken in t, and the boxes need padding only for the errors that do not grow with the distance (rtg_api.cpp
-// culling_box). Sphere-only kernels keep the plain compare (their boxes carry the distance terms).
-constexpr float kCullWiden = 1.0f + 0x1p-20f;
+// Kernels that test quads compare a child's entry distance with min(exit, tbest) * kCullWiden instead: the
+// slab test's relative error (3 2^-24 of t per plane) and quad_t's (2 2^-24) are then taken in t, so the boxes
+// need padding only for the errors that do not grow with the distance (rtg_api.cpp culling_box), and the
+// factor is the cull bound's relative margin as well (its absolute 2^-19 is covered by the pads there). One
+// v_pk_mul_f32 per child pair replaces cull_bound. Sphere-only kernels keep cull_bound and the plain exit
+// (their boxes carry the distance terms).
+constexpr float kCullWiden = 1.0f + 0x1p-19f;
 constexpr float kPi = 3.14159265358979323846f;
 constexpr int kMaxTexNesting = 16;
 
@@ -476,11 +478,10 @@ __device__ __forceinline__ uint32_t child_key(float tnx, float tny, float tnz, f
   // tn >= kCullTMin > 0, so its bits order like the float; the low 4 bits carry the slot (x4)
   return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
-// the same with the exit distance tf already formed (the far planes' minimum times kCullWiden: quad kernels)
-__device__ __forceinline__ uint32_t child_key_exit(float tnx, float tny, float tnz, float tf, float tc,
-                                                   uint32_t slot) {
+// the same with the bound already formed (quad kernels: min(exit, tbest) * kCullWiden)
+__device__ __forceinline__ uint32_t child_key_exit(float tnx, float tny, float tnz, float tf, uint32_t slot) {
   const float tn = fmaxf(fmaxf(fmaxf(tnx, tny), tnz), kCullTMin);
-  return tn <= fminf(tf, tc) ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
+  return tn <= tf ? ((static_cast<uint32_t>(ibits(tn)) & ~15u) | slot) : ~0u;
 }
 
 __device__ __forceinline__ void psort(uint32_t& ka, int32_t& ca, uint32_t& kb, int32_t& cb) {
@@ -561,18 +562,19 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   const f2 fx01 = pk_fma(f2{fx.x, fx.y}, ix, ox), fx23 = pk_fma(f2{fx.z, fx.w}, ix, ox);
   const f2 fy01 = pk_fma(f2{fy.x, fy.y}, iy, oy), fy23 = pk_fma(f2{fy.z, fy.w}, iy, oy);
   const f2 fz01 = pk_fma(f2{fz.x, fz.y}, iz, oz), fz23 = pk_fma(f2{fz.z, fz.w}, iz, oz);
-  const float tc = cull_bound(t.tbest);
   uint32_t k0, k1, k2, k3;
-  if constexpr (WIDEN) {  // one v_pk_mul_f32 per child pair
-    const f2 tf01 = f2{fminf(fminf(fx01.x, fy01.x), fz01.x), fminf(fminf(fx01.y, fy01.y), fz01.y)} *
+  if constexpr (WIDEN) {  // min(exit, tbest) * kCullWiden: one v_pk_mul_f32 per child pair, no cull_bound
+    const float tb = t.tbest;
+    const f2 tf01 = f2{fminf(fminf(fminf(fx01.x, fy01.x), fz01.x), tb), fminf(fminf(fminf(fx01.y, fy01.y), fz01.y), tb)} *
                     f2{kCullWiden, kCullWiden};
-    const f2 tf23 = f2{fminf(fminf(fx23.x, fy23.x), fz23.x), fminf(fminf(fx23.y, fy23.y), fz23.y)} *
+    const f2 tf23 = f2{fminf(fminf(fminf(fx23.x, fy23.x), fz23.x), tb), fminf(fminf(fminf(fx23.y, fy23.y), fz23.y), tb)} *
                     f2{kCullWiden, kCullWiden};
-    k0 = child_key_exit(nx01.x, ny01.x, nz01.x, tf01.x, tc, 0);
-    k1 = child_key_exit(nx01.y, ny01.y, nz01.y, tf01.y, tc, 4);
-    k2 = child_key_exit(nx23.x, ny23.x, nz23.x, tf23.x, tc, 8);
-    k3 = child_key_exit(nx23.y, ny23.y, nz23.y, tf23.y, tc, 12);
+    k0 = child_key_exit(nx01.x, ny01.x, nz01.x, tf01.x, 0);
+    k1 = child_key_exit(nx01.y, ny01.y, nz01.y, tf01.y, 4);
+    k2 = child_key_exit(nx23.x, ny23.x, nz23.x, tf23.x, 8);
+    k3 = child_key_exit(nx23.y, ny23.y, nz23.y, tf23.y, 12);
   } else {
+    const float tc = cull_bound(t.tbest);
     k0 = child_key(nx01.x, ny01.x, nz01.x, fx01.x, fy01.x, fz01.x, tc, 0);
     k1 = child_key(nx01.y, ny01.y, nz01.y, fx01.y, fy01.y, fz01.y, tc, 4);
     k2 = child_key(nx23.x, ny23.x, nz23.x, fx23.x, fy23.x, fz23.x, tc, 8);

@@ -567,14 +567,18 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->depth = 0;
     out->stack_need = 0;
   } else if (d->bvh_mode == RTG_BVH_SAH && !bvh.nodes.empty()) {
-    // 4-wide collapse: SAH-optimal (dynamic program, wide-node visit = 1 primitive test, leaves <= 4)
-    // by default: Cornell 800x800 2000 spp -2.7 % (box tests 12.7 -> 9.4 per segment), book-1 and
-    // the 1M-sphere field unchanged (profiles/r03_e). RTG_COLLAPSE="greedy" keeps round 2's greedy
-    // collapse, "sah:c_node:max_leaf" other constants (A/B)
+    // 4-wide collapse: SAH-optimal (dynamic program, leaves <= 4) by default: Cornell 800x800 2000 spp
+    // -2.7 % against the greedy collapse (box tests 12.7 -> 9.4 per segment), book-1 and the 1M-sphere
+    // field unchanged (profiles/r03_e). A wide-node visit is priced as half a primitive test since round
+    // 5: with one primitive per leaf trip a quad test costs a trip of its own, and Cornell's tree at 0.5
+    // (single-quad leaves: box tests 9.48 -> 10.59, quad tests 1.61 -> 1.22 per segment) is 8 % faster
+    // than at 1.0; book-1 and the 1M field within 0.3 % (profiles/r05_s ... r05_u). RTG_COLLAPSE="greedy"
+    // keeps round 2's greedy collapse, "sah:c_node:max_leaf" other constants (A/B)
     CollapseParams cp;
     cp.sah = true;
+    cp.c_node = 0.5;
     if (const char* e = std::getenv("RTG_COLLAPSE")) {
-      double cn = 1.0;
+      double cn = 0.5;
       int ml = 4;
       if (std::strncmp(e, "greedy", 6) == 0) {
         cp.sah = false;

@@ -637,7 +637,7 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
 // Test the first primitive of a leaf (t.todo < 0): the lane stays at the rest of the leaf (first + 1,
 // count - 1) for its next leaf trip, or pops after the last. One primitive per lane per trip keeps the
 // leaf trip's lanes in step (a loop over each lane's own count ran as long as the wave's largest leaf):
-// config 2 -0.9 %, config 5 -0.7 %, Cornell +-0, frames identical. The lane's
+// config 2 -0.5 %, config 5 -0.4 %, Cornell +0.3 %, frames identical. The lane's
 // primitives are tested in the same order as before, so ties resolve the same way. CHECK: validate the
 // leaf code (off in the LDS schedule outside the COUNT diagnostics, as for node codes).
 template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,

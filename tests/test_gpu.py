@@ -674,6 +674,26 @@ def test_near_tie_culling_is_conservative(gpu_lib, oracle, bvh, competitor):
         assert np.array_equal(g, o) and st.segments == segs, (h, colour_counts(g), colour_counts(o))
 
 
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
+@pytest.mark.parametrize("offset", [0.0, 3000.0])
+def test_quad_edges_culling_is_conservative(gpu_lib, oracle, bvh, offset):
+    """Per-primitive culling boxes (DESIGN.md §4 "conservative culling", round 5): a room of quads meeting at
+    shared edges — axis-aligned walls and blocks (thin flat-axis pads, extent-aware in-plane pads, exits
+    widened in the quad kernel), blocks rotated about skew axes and quads rotated within their plane (the
+    general 2^-18 pads), spheres on top — rendered at 8 spp, depth 8, near the origin and translated 3000
+    units away, with every BVH builder: every pixel and the segment count are cpu_ref32's."""
+    from tie_scene import quad_edge_scene
+
+    d, cam = quad_edge_scene(bvh, width=96, offset=offset)
+    ds = gpu_lib.scene_create(d)
+    g, st = ds.render_host(cam)
+    ds.close()
+    o, segs = oracle.render_f32(d, cam, threads=_host_threads())
+    assert float(np.mean(o > 0)) > 0.5
+    assert np.array_equal(g, o) and st.segments == segs, (float(np.mean(np.all(g == o, axis=-1))), st.segments,
+                                                          segs)
+
+
 def test_traversal_stack_spill_matches_oracle(gpu_lib, scenes, oracle, monkeypatch):
     """Deep BVHs keep the first stack entries in LDS and the rest in a global per-wave spill area
     (the 1M-sphere scene needs 36 entries). RTG_STACK_LDS_ENTRIES lowers the LDS part so that the

@@ -125,3 +125,67 @@ def near_tie_scene(bvh_mode=rtgpu.RTG_BVH_SAH, competitor="quad", width=64, cam_
                        lookat=(0.0, y0, 0.0), vup=(0.0, 0.0, 1.0),
                        vfov=float(np.degrees(2 * np.arctan(half / cam_height))), focus_dist=cam_height)
     return make_desc(prims, mat, tex, bvh_mode), cam
+
+
+def _quad(m, Q, u, v):
+    return rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_QUAD, material=m, p0=rtgpu.D3(*Q), p1=rtgpu.D3(*u),
+                               p2=rtgpu.D3(*v))
+
+
+def _box_quads(m, lo, hi, R=None, pivot=(0.0, 0.0, 0.0)):
+    """The six faces of a box as quads sharing their edges (as the reference's box(), quad.hpp), optionally
+    rotated by the 3x3 matrix R about `pivot`."""
+    import numpy as np
+
+    lo, hi = np.asarray(lo, float), np.asarray(hi, float)
+    dx, dy, dz = np.array([hi[0] - lo[0], 0, 0]), np.array([0, hi[1] - lo[1], 0]), np.array([0, 0, hi[2] - lo[2]])
+    faces = [(lo, dy, dz), (lo + dx, dy, dz), (lo, dx, dz), (lo + dy, dx, dz), (lo, dx, dy), (lo + dz, dx, dy)]
+    out = []
+    for Q, u, v in faces:
+        if R is not None:
+            p = np.asarray(pivot, float)
+            Q, u, v = R @ (Q - p) + p, R @ u, R @ v
+        out.append(_quad(m, tuple(float(x) for x in Q), tuple(float(x) for x in u), tuple(float(x) for x in v)))
+    return out
+
+
+def quad_edge_scene(bvh_mode=rtgpu.RTG_BVH_SAH, width=64, offset=0.0, spp=8, seed=7):
+    """Quads meeting at shared edges (DESIGN.md §4 "conservative culling", round 5): an open room of
+    axis-aligned walls, axis-aligned blocks standing on its floor and against a wall, blocks rotated about
+    skew axes (no flat axis: every plane padded by 2^-18 (|v| + M)), quads flat in z but rotated within
+    their plane (u, v not along the axes: treated as general quads), small spheres resting on block tops
+    and a ceiling light, the whole scene translated by `offset` along every axis (|v| + M large against the
+    room's size). Rays leave faces at every angle and graze their neighbours' edges, which is where the
+    per-axis culling boxes and the widened exits have to hold."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    tex = [rtgpu.rtg_texture(type=rtgpu.RTG_TEX_SOLID, color=rtgpu.D3(*c))
+           for c in ((0.73, 0.73, 0.73), (0.65, 0.05, 0.05), (0.12, 0.45, 0.15), (15.0, 15.0, 15.0))]
+    mat = [rtgpu.rtg_material(type=rtgpu.RTG_MAT_LAMBERTIAN, texture=k) for k in range(3)]
+    mat.append(rtgpu.rtg_material(type=rtgpu.RTG_MAT_DIFFUSE_LIGHT, texture=3))
+    o = np.array([offset, offset, offset])
+    S = 20.0
+    t = lambda *p: tuple(float(x) for x in np.asarray(p, float) + o)
+    prims = [_quad(2, t(S, 0, 0), (0, S, 0), (0, 0, S)), _quad(1, t(0, 0, 0), (0, S, 0), (0, 0, S)),
+             _quad(0, t(0, 0, 0), (S, 0, 0), (0, 0, S)), _quad(0, t(S, S, S), (-S, 0, 0), (0, 0, -S)),
+             _quad(0, t(0, 0, S), (S, 0, 0), (0, S, 0)), _quad(3, t(17, S - 0.01, 17), (-14, 0, 0), (0, 0, -14))]
+    prims += _box_quads(0, t(3, 0, 3), t(9, 6, 9))      # on the floor
+    prims += _box_quads(1, t(12, 0, 14), t(S, 10, S))   # in the back corner, flush with two walls
+    for k in range(3):  # rotated about skew axes
+        axis = rng.normal(size=3)
+        axis /= np.linalg.norm(axis)
+        a = rng.uniform(0.3, 1.2)
+        K = np.array([[0, -axis[2], axis[1]], [axis[2], 0, -axis[0]], [-axis[1], axis[0], 0]])
+        R = np.eye(3) + np.sin(a) * K + (1 - np.cos(a)) * (K @ K)
+        c = np.array([4.0 + 6.0 * k, 12.0, 6.0 + 3.0 * k])
+        prims += _box_quads(k % 3, t(*(c - 1.5)), t(*(c + 1.5)), R, pivot=t(*c))
+    for k in range(3):  # flat in z, rotated within the plane
+        a = rng.uniform(0.2, 1.3)
+        u = (3.0 * np.cos(a), 3.0 * np.sin(a), 0.0)
+        v = (-2.0 * np.sin(a), 2.0 * np.cos(a), 0.0)
+        prims.append(_quad(k % 3, t(5.0 + 4.0 * k, 3.0 + 2.0 * k, 12.0), u, v))
+    prims += [_sphere(1, t(6, 7, 6), 1.0), _sphere(2, t(16, 11.5, 17), 1.5)]
+    cam = rtgpu.camera(image_width=width, aspect_ratio=1.0, samples_per_pixel=spp, max_depth=8,
+                       background=(0.0, 0.0, 0.0), lookfrom=t(10, 10, -18), lookat=t(10, 9, 10), vfov=55.0)
+    return make_desc(prims, mat, tex, bvh_mode), cam

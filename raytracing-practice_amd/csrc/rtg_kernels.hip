@@ -634,14 +634,15 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
-// Test the first primitive of a leaf (t.todo < 0): the lane stays at the rest of the leaf (first + 1,
-// count - 1) for its next leaf trip, or pops after the last. One primitive per lane per trip keeps the
-// leaf trip's lanes in step (a loop over each lane's own count ran as long as the wave's largest leaf):
-// config 2 -0.5 %, config 5 -0.4 %, Cornell +0.3 %, frames identical. The lane's
-// primitives are tested in the same order as before, so ties resolve the same way. CHECK: validate the
-// leaf code (off in the LDS schedule outside the COUNT diagnostics, as for node codes).
+// Test the primitives of a leaf (t.todo < 0). ONE (the LDS schedule): only the first, and the lane stays at
+// the rest of the leaf (first + 1, count - 1) for its next leaf trip, or pops after the last: one primitive
+// per lane per trip keeps the leaf trip's lanes in step (a loop over each lane's own count runs as long as
+// the wave's largest leaf): config 2 -0.5 %, Cornell +0.3 %, frames identical. The treelet schedule loops
+// over the leaf and pops (config 5 at full size: one per trip +1.4 %). Either way a
+// lane tests its primitives in the same order, so ties resolve the same way. CHECK: validate the leaf code
+// (off in the LDS schedule outside the COUNT diagnostics, as for node codes).
 template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,
-          int PRIMS = kPrimsAny>
+          int PRIMS = kPrimsAny, bool ONE = GEOM == kGeomLds>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
   auto pop = [&]() { trav_pop(t, stk); };
@@ -654,24 +655,24 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     return;
   }
   if ((PRIMS & kPrimsKind) == kPrimsSpheres || ((PRIMS & kPrimsKind) == kPrimsAny && S.ref_mode == 1)) {  // sphere-only scene, primitives stored in reference order
-    {
-      const float4* sp4 = S.spheres + static_cast<int64_t>(first) * S.sphere_f4;
+    for (int k = 0; k < (ONE ? 1 : count); ++k) {
+      const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
-      const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first == t.origin);
+      const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
       if (th > 0.0f) {  // sphere_t: th < tbest
         t.tbest = th;
-        t.best = first;
+        t.best = first + k;
         t.mat = MAT ? ibits(sp4[1].w) : -1;
       }
     }
-    if (count > 1)
+    if (ONE && count > 1)
       t.todo = ~(((first + 1) << 3) | (count - 2));
     else
       pop();
     return;
   }
-  {
-    const int32_t ref = S.ref_mode == 0 ? S.refs[first] : (first | kQuadRefBit);
+  for (int k = 0; k < (ONE ? 1 : count); ++k) {
+    const int32_t ref = S.ref_mode == 0 ? S.refs[first + k] : ((first + k) | kQuadRefBit);
     float th;
     if (COUNT) cnt.prim += 1;
     int32_t m = 0, qrank = -1;
@@ -700,7 +701,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       t.mat = MAT ? m : qrank;
     }
   }
-  if (count > 1)
+  if (ONE && count > 1)
     t.todo = ~(((first + 1) << 3) | (count - 2));
   else
     pop();

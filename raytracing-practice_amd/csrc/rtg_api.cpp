@@ -50,7 +50,11 @@ constexpr int kSmallBvhNodes = 16;
 constexpr int kSmallBvhLeafBatch = 16;
 constexpr int kLdsWaves = 16;           // persistent LDS workgroup size (rtg_kernels.hip)
 constexpr int kSmallSceneWgs = 5;       // 4-wave persistent workgroups per CU for small scenes
-constexpr int64_t kRingAutoBytes = int64_t(4) << 30;  // full-frame partials above this: the tile ring
+// full-frame partials above this: the tile ring. 32 GiB of the MI355X's 288 GB: config 5's 6.3 GB of partials
+// (4K, 63 chunks) stay full-frame since round 5 — its render loop is 2.0 % faster without the ring's
+// bookkeeping and its HBM writes drop from 16.3 GB (ring slots + the ring kernel's scratch) to the
+// partials' 6.3 GB (profiles/r05_dd, r05_final); the ring remains for frames whose partials would not fit
+constexpr int64_t kRingAutoBytes = int64_t(32) << 30;
 constexpr int kNumCounters = 28;        // see DevJob::counters ([8..23] diagnostics, [24..25] tile ring, [26] stack spills)
 // gfx950 allocates a workgroup's LDS in 1280-byte granules (160 KB = 128 of them): measured with the
 // dual launch, whose two workgroups stop sharing a CU exactly when the rounded sizes pass 160 KB
@@ -1298,8 +1302,8 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
 
   // one-shot chunked frames of the default schedules sum each tile's chunks through the tile ring
   // (RING kernels; the counting kernels keep the full-frame partials, same frame)
-  // By default only where the full-frame partial buffers would be large (config 5's 6.3 GB): the ring
-  // costs the render loop time (config 5 +2.8 %, config 2 +7.5 %, config 4 +17 %: DESIGN.md §9), the
+  // By default only where the full-frame partial buffers would be very large (kRingAutoBytes): the ring
+  // costs the render loop time (config 5 +2.0 %, config 2 +7.5 %, config 4 +17 %: DESIGN.md §9), the
   // full-frame buffers cost memory. RTG_TILE_SLOTS=0 / >0 forces it off / on.
   const int64_t full_partial_bytes = int64_t(rows) * W * 12 * dj.chunks;
   const bool ring_on = K.tile_slots > 0 || (K.tile_slots < 0 && full_partial_bytes > kRingAutoBytes);

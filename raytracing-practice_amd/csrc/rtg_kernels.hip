@@ -634,15 +634,15 @@ __device__ __forceinline__ void node_step4(Trav& t, const DevScene& S, const Stk
   }
 }
 
-// Test the primitives of a leaf (t.todo < 0). ONE (the LDS schedule): only the first, and the lane stays at
-// the rest of the leaf (first + 1, count - 1) for its next leaf trip, or pops after the last: one primitive
-// per lane per trip keeps the leaf trip's lanes in step (a loop over each lane's own count runs as long as
-// the wave's largest leaf): config 2 -0.5 %, Cornell +0.3 %, frames identical. The treelet schedule loops
-// over the leaf and pops (config 5 at full size: one per trip +1.4 %). Either way a
-// lane tests its primitives in the same order, so ties resolve the same way. CHECK: validate the leaf code
-// (off in the LDS schedule outside the COUNT diagnostics, as for node codes).
+// Test the primitives of a leaf (t.todo < 0). ONE: only the first, and the lane stays at the rest of the leaf
+// (first + 1, count - 1) for its next leaf trip, or pops after the last: one primitive per lane per trip
+// keeps the leaf trip's lanes in step (a loop over each lane's own count runs as long as the wave's largest
+// leaf): config 2 -0.5 %, config 5 -0.4 %, Cornell +0.3 %, frames identical. The tile-ring kernels of the
+// cache-read schedules loop over the leaf and pop (config 5 with the ring: one per trip +1.4 %; DESIGN.md §8
+// round 5). Either way a lane tests its primitives in the same order, so ties resolve the same way. CHECK:
+// validate the leaf code (off in the LDS schedule outside the COUNT diagnostics, as for node codes).
 template <class Stk, bool COUNT, bool CHECK = true, bool MAT = false, int WIDE = 4, int GEOM = kGeomLds,
-          int PRIMS = kPrimsAny, bool ONE = GEOM == kGeomLds>
+          int PRIMS = kPrimsAny, bool ONE = true>
 __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d, float time,
                                           const Stk& stk, Counts<COUNT>& cnt, bool& corrupt) {
   auto pop = [&]() { trav_pop(t, stk); };
@@ -1345,8 +1345,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         }
       }
       if (leaf_trip && tr.todo < 0)
-        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM, PRIMS>(tr, S, ps.o, ps.d, ps.time, stk, w.cnt,
-                                                                           w.corrupt);
+        leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM, PRIMS, GEOM == kGeomLds || !RING>(
+            tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip

@@ -380,7 +380,7 @@ def test_sample_chunks_match_oracle(gpu_lib, scenes, oracle, spp):
 def test_tile_ring_matches_full_frame_partials(gpu_lib, scenes, name, W, spp, schedule, monkeypatch):
     """One-shot chunked frames can sum each tile's chunks in chunk order in the wave whose batch of the
     tile finished last, through a ring of tile slots (DESIGN.md §4 "per-tile combine"; the default
-    above 4 GiB of full-frame partials). The frame and the segment count must be those of the
+    above 32 GiB of full-frame partials). The frame and the segment count must be those of the
     full-frame partial buffers + combine kernel (RTG_TILE_SLOTS=0) for a ring with a slot per tile
     and for rings of 1, 2 and 8 slots, where nearly every batch finds its slot still owned by an
     earlier tile and waits (book-1: the dual launch; Cornell: 4-wave workgroups; schedule 5: the
@@ -463,7 +463,7 @@ def test_tile_ring_on_strided_shards(gpu_lib, scenes, schedule, world, monkeypat
 def test_tile_ring_bounds_fall_back_to_full_frame(gpu_lib, scenes):
     """The ring kernels index the shard's frame with 32-bit byte offsets: a shard of >= 2 GiB (here
     18432 x 10368 px x 12 B) keeps the full-frame partials even where the ring would be the default
-    (above 4 GiB of partials); just below the bound the ring is chosen (plans only, nothing rendered)."""
+    (above 32 GiB of partials); just below the bound the ring is chosen (plans only, nothing rendered)."""
     s = scenes.build("bouncing_spheres", rand_seed=1)
     c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
     c.samples_per_pixel, c.max_depth = 1000, 50
@@ -1062,13 +1062,24 @@ def test_render_plan_names_the_kernel(gpu_lib, scenes, name, grid, W, schedule, 
     assert 0 < p.vgprs <= 512 // waves_per_simd and p.chunks == 32 and p.chunk_samples == 16
     assert p.num_cus > 0 and p.workgroups > 0
     H = gpu_lib.camera_resolve(c).image_height
-    assert p.tile_slots == 0 and p.partial_bytes == H * W * 12 * 32, p.as_dict()  # < 4 GiB: full-frame
-    if grid == 500:  # config 5 as benchmarked (1000 spp): 6.3 GB of full-frame partials -> the tile
-        # ring, ~2^17 batches of 1 KiB (R * chunks) plus 8 B of slot words per slot
+    assert p.tile_slots == 0 and p.partial_bytes == H * W * 12 * 32, p.as_dict()  # < 32 GiB: full-frame
+    if grid == 500:  # config 5 as benchmarked (1000 spp): 6.3 GB of full-frame partials, below the tile
+        # ring's 32 GiB default bound since round 5; forced on, the ring holds ~2^17 batches of 1 KiB
+        # (R * chunks) plus 8 B of slot words per slot
         c.samples_per_pixel = 1000
         ds = gpu_lib.scene_create(s.desc)
         p = ds.plan(c)
+        assert p.chunks == 63 and p.tile_slots == 0 and p.partial_bytes == H * W * 12 * 63, p.as_dict()
         ds.close()
+        import os
+
+        os.environ["RTG_TILE_SLOTS"] = "2048"
+        try:
+            ds = gpu_lib.scene_create(s.desc)
+            p = ds.plan(c)
+            ds.close()
+        finally:
+            del os.environ["RTG_TILE_SLOTS"]
         assert p.chunks == 63 and p.tile_slots == 2048, p.as_dict()
         assert p.partial_bytes == 2048 * 63 * 1024 + 8 * 2048 < H * W * 12 * 63 // 40
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""tools/diff_pixels.py — which of two library builds is right where their frames differ.
+"""tests/tools/diff_pixels.py — which of two library builds is right where their frames differ.
 
-  python3 tools/diff_pixels.py --libs new=PATH,old=PATH [--scene S --grid G --width W --height H --spp N
+  python3 tests/tools/diff_pixels.py --libs new=PATH,old=PATH [--scene S --grid G --width W --height H --spp N
                                --depth D --threads T]
 
 Renders one frame with each build (same box, same seed), lists the pixels where the two differ, renders
@@ -15,7 +15,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "raytracing-practice_amd", "python"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""tools/full_frame_check.py — one benchmark frame at its full size AND full spp, every pixel against the
+"""tests/tools/full_frame_check.py — one benchmark frame at its full size AND full spp, every pixel against the
 oracle (a checker: cpu_ref32 from oracle/, test infrastructure).
 
-  python3 tools/full_frame_check.py [--scene S --grid G --width W --height H --spp N --depth D]
+  python3 tests/tools/full_frame_check.py [--scene S --grid G --width W --height H --spp N --depth D]
                                     [--threads T] [--block R] [--rows-from A --rows-to B]
 
 Renders the frame once with the library, then renders it with cpu_ref32 in blocks of R rows on T host
@@ -17,7 +17,7 @@ import time
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "raytracing-practice_amd", "python"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""tools/near_tie_probe.py — pixels where a build's near-tie frame (tests/tie_scene.py near_tie_scene)
+"""tests/tools/near_tie_probe.py — pixels where a build's near-tie frame (tests/tie_scene.py near_tie_scene)
 differs from cpu_ref32, over camera heights, competitors and BVH builders; for choosing a test scene that
 the pre-round-5 culling fails (a negative control) and the current one passes."""
 import json
@@ -8,7 +8,7 @@ import sys
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "raytracing-practice_amd", "python"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 

@@ -195,6 +195,7 @@ __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
 constexpr float kSphereF64Radius = 16.0f;
 // a = d.d and inv_a = 1/a (correctly rounded) are per ray (Trav): the far root is q * inv_a and
 // only the near root c / q is a division.
+template <bool INCL = false>
 __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, float a, float inv_a, float time,
                                           float tmin, float tmax, bool origin) {
   const V3 C = madd(time, xyz(s1), xyz(s0));
@@ -229,12 +230,11 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
   const float t1 = div_rn(c, q);
   const float lo = fminf(t0, t1);
   const float hi = fmaxf(t0, t1);
-  // roots strictly inside (tmin, tmax), interval::surrounds (sphere.hpp:70): a sphere never replaces an
-  // equal-t hit; two spheres at the bit-identical t keep the one tested first (DESIGN.md §4 "tie rule": the
-  // list-order form for spheres was measured and rejected in round 5, tools/experiments/sphere_tie_rule.patch)
-  if (origin) return (hb < 0.0f && tmin < hi && hi < tmax) ? hi : -1.0f;
-  if (tmin < lo && lo < tmax) return lo;
-  if (tmin < hi && hi < tmax) return hi;
+  // roots inside (tmin, tmax), interval::surrounds (sphere.hpp:70); INCL: (tmin, tmax], so that the leaf test
+  // sees a root equal to the closest hit and applies the exact-t tie rule (DESIGN.md §4 "tie rule")
+  if (origin) return (hb < 0.0f && tmin < hi && (INCL ? hi <= tmax : hi < tmax)) ? hi : -1.0f;
+  if (tmin < lo && (INCL ? lo <= tmax : lo < tmax)) return lo;
+  if (tmin < hi && (INCL ? hi <= tmax : hi < tmax)) return hi;
   return -1.0f;
 }
 
@@ -277,13 +277,14 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // closest_so_far (interval::contains, quad.hpp:62, interval.hpp:29), sphere::hit does not
 // (interval::surrounds, sphere.hpp:70, interval.hpp:32). So among the primitives at the smallest t it
 // keeps the last quad of the list if there is one, else the first sphere, whatever order they are tested
-// in. The kernels test in BVH order: sphere_t returns roots strictly below tmax (a sphere never replaces an
-// equal-t hit), quad_t roots up to tmax, and a quad root equal to the closest hit replaces it only if that
-// hit is a sphere or an earlier quad of the list (S.tie_rank: each quad slot's list index, read only on a
-// tie; the check is one compare and a wave-uniform branch). Two spheres at the bit-identical t keep the one
-// tested first: the one order-dependent case. Its list-order form (round 5) cost config 2 +3.5 %, config 3
-// +8.5 %, config 5 +1.1 % in register allocation for the 14 pixels of 10 M it decides at full spp in
-// configs 2 and 5 (tools/experiments/sphere_tie_rule.patch).
+// in. The kernels test in BVH order: quad_t returns roots up to tmax, and a quad root equal to the closest
+// hit replaces it only if that hit is a sphere or an earlier quad of the list (S.tie_rank: each slot's list
+// index, read only on a tie; the check is one compare and a wave-uniform branch); the leaf tests take sphere
+// roots up to tmax too (sphere_t<true>), and a sphere root equal to the closest hit replaces it only if that
+// hit is a sphere later in the list, again with the ranks read only on a tie. The sphere half (round 5)
+// decides 14 pixels of the 10 M of configs 2 and 5 at full spp for config 2 +0.9 %, config 5 +0.6 %
+// (earlier forms that carried ranks through the loop cost 2-8 %: tools/experiments/sphere_tie_rule.patch;
+// DESIGN.md §4, §8).
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
@@ -658,8 +659,13 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
     for (int k = 0; k < (ONE ? 1 : count); ++k) {
       const float4* sp4 = S.spheres + static_cast<int64_t>(first + k) * S.sphere_f4;
       if (COUNT) cnt.prim += 1;
-      const float th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
-      if (th > 0.0f) {  // sphere_t: th < tbest
+      const float th = sphere_t<true>(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
+      // exact-t tie (rare; a wave-uniform branch): the sphere earlier in the list wins, as the reference's list
+      // walk keeps the first sphere at a t (interval::surrounds); the ranks are read only then
+      bool take = th > 0.0f && th < t.tbest;
+      if (ballot_tie(th == t.tbest) != 0 && th == t.tbest)
+        take = S.tie_rank[first + k] < S.tie_rank[t.best];
+      if (take) {
         t.tbest = th;
         t.best = first + k;
         t.mat = MAT ? ibits(sp4[1].w) : -1;
@@ -691,9 +697,12 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       }
     } else {
       const float4* sp4 = S.spheres + static_cast<int64_t>(ref) * S.sphere_f4;
-      th = sphere_t(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
+      th = sphere_t<true>(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, ref == t.origin);
       if (MAT) m = ibits(sp4[1].w);
-      take = th > 0.0f;  // sphere_t: th < tbest
+      take = th > 0.0f && th < t.tbest;
+      // exact-t tie: a sphere replaces only an equal-t sphere later in the list (never a quad)
+      if (ballot_tie(th == t.tbest) != 0 && th == t.tbest)
+        take = !(t.best & kQuadRefBit) && S.tie_rank[ref] < S.tie_rank[t.best];
     }
     if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;

@@ -286,6 +286,15 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // (earlier forms that carried ranks through the loop cost 2-8 %: tools/experiments/sphere_tie_rule.patch;
 // DESIGN.md §4, §8).
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+// S.tie_rank for the sphere tie rule, read from the kernel arguments at the (rare) tie itself: every kernel
+// that runs leaf_step (render_kernel, render_kernel_lds) takes its DevScene as the first argument. A volatile
+// load there keeps the pointer out of the SGPRs live across the trip loop; with S.tie_rank instead the
+// compiler held it from the kernel's start and spilled other scalars to VGPR lanes (config 2 +0.7 %,
+// config 3 +4.5 %, config 5 +1.2 %, frames identical)
+__device__ __forceinline__ const int32_t* tie_ranks_late() {
+  const volatile DevScene* ks = (const volatile DevScene*)(__builtin_amdgcn_kernarg_segment_ptr());
+  return ks->tie_rank;
+}
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
@@ -661,10 +670,10 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       if (COUNT) cnt.prim += 1;
       const float th = sphere_t<true>(sp4[0], sp4[1], o, d, t.a, t.inv_a, time, kTMin, t.tbest, first + k == t.origin);
       // exact-t tie (rare; a wave-uniform branch): the sphere earlier in the list wins, as the reference's list
-      // walk keeps the first sphere at a t (interval::surrounds); the ranks are read only then
+      // walk keeps the first sphere at a t (interval::surrounds); the ranks are read only then (tie_ranks_late)
       bool take = th > 0.0f && th < t.tbest;
       if (ballot_tie(th == t.tbest) != 0 && th == t.tbest)
-        take = S.tie_rank[first + k] < S.tie_rank[t.best];
+        take = tie_ranks_late()[first + k] < tie_ranks_late()[t.best];
       if (take) {
         t.tbest = th;
         t.best = first + k;
@@ -702,7 +711,7 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       take = th > 0.0f && th < t.tbest;
       // exact-t tie: a sphere replaces only an equal-t sphere later in the list (never a quad)
       if (ballot_tie(th == t.tbest) != 0 && th == t.tbest)
-        take = !(t.best & kQuadRefBit) && S.tie_rank[ref] < S.tie_rank[t.best];
+        take = !(t.best & kQuadRefBit) && tie_ranks_late()[ref] < tie_ranks_late()[t.best];
     }
     if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;

@@ -281,10 +281,9 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
 // hit replaces it only if that hit is a sphere or an earlier quad of the list (S.tie_rank: each slot's list
 // index, read only on a tie; the check is one compare and a wave-uniform branch); the leaf tests take sphere
 // roots up to tmax too (sphere_t<true>), and a sphere root equal to the closest hit replaces it only if that
-// hit is a sphere later in the list, again with the ranks read only on a tie. The sphere half (round 5)
-// decides 14 pixels of the 10 M of configs 2 and 5 at full spp for config 2 +0.9 %, config 5 +0.6 %
-// (earlier forms that carried ranks through the loop cost 2-8 %: tools/experiments/sphere_tie_rule.patch;
-// DESIGN.md §4, §8).
+// hit is a sphere later in the list, again with the ranks read only on a tie (tie_ranks_late). The sphere
+// half (round 5) decides 14 pixels of the 10 M of configs 2 and 5 at full spp at no net cost (earlier forms
+// that carried ranks through the loop cost 2-8 %: tools/experiments/sphere_tie_rule.patch).
 __device__ __forceinline__ uint64_t ballot_tie(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // S.tie_rank for the sphere tie rule, read from the kernel arguments at the (rare) tie itself: every kernel
 // that runs leaf_step (render_kernel, render_kernel_lds) takes its DevScene as the first argument. A volatile

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 6
+#define RTG_ABI_VERSION 7
 
 typedef int32_t rtg_status;
 #define RTG_OK 0
@@ -105,10 +105,10 @@ typedef struct rtg_perlin {
                             milliseconds for 1M primitives, more traversal steps than SAH */
 
 typedef struct rtg_scene_desc {
-  uint32_t abi_version; /* RTG_ABI_VERSION */
+  uint32_t abi_version; /* RTG_ABI_VERSION (6 is still accepted: it has no tie_rank, read as NULL) */
   int32_t bvh_mode;     /* RTG_BVH_* */
   const rtg_primitive* prims;
-  int64_t num_prims; /* object order == hittable_list order (tie-breaking, H9) */
+  int64_t num_prims; /* object order == hittable_list order */
   const rtg_material* materials;
   int32_t num_materials;
   int32_t num_textures;
@@ -117,6 +117,13 @@ typedef struct rtg_scene_desc {
   int32_t num_images;
   int32_t num_perlins;
   const rtg_perlin* perlins;
+  /* ABI 7. Exact-t ties (H9): the reference's closest-hit walk keeps the first sphere and the last quad
+   * hit at the smallest t (interval::surrounds, sphere.hpp:70; interval::contains, quad.hpp:62) in the
+   * order it tests objects: a hittable_list in list order (hittable_list.hpp:40-64), a bvh_node left
+   * then right (bvh_node.hpp:89-90), i.e. its children in the median tree's leaf order, not the list's.
+   * tie_rank[i] = primitive i's position in that order, a permutation of 0..num_prims-1 (the C++
+   * mirror's bvh_node fills it from rtg_bvh_node_order); NULL = the primitive order itself. */
+  const int64_t* tie_rank;
 } rtg_scene_desc;
 
 /* ---- camera: the reference's public fields (camera.hpp:13-25) ---- */
@@ -416,6 +423,15 @@ typedef struct rtg_bvh_node_host {
 rtg_status rtg_bvh_build_host(const rtg_scene_desc* desc, rtg_bvh_node_host* nodes_out,
                               int64_t max_nodes, int64_t* refs_out, int64_t max_refs,
                               int64_t* num_nodes, int64_t* num_refs, int32_t* depth);
+
+/* Host-only (ABI 7): the order in which bvh_node(objects, 0, n) (bvh_node.hpp:25-77) leaves `objects`
+ * — its leaves left to right, the order bvh_node::hit (bvh_node.hpp:80-94) tests them in. boxes holds
+ * each object's bounding_box() as {lo.x, lo.y, lo.z, hi.x, hi.y, hi.z} (n x 6 doubles, list order);
+ * order receives n list indices. The reference's own steps: range box, aabb::longest_axis, std::sort
+ * by box min on that axis (libstdc++'s, so objects with equal keys land where the reference's land),
+ * median split, no sort for spans of 1 or 2. Replaces nothing on the device path: the C++ mirror's
+ * bvh_node uses it to fill rtg_scene_desc.tie_rank. */
+rtg_status rtg_bvh_node_order(const double* boxes, int64_t n, int64_t* order);
 
 #ifdef __cplusplus
 }

@@ -949,13 +949,18 @@ static float quad_t32(const float* q, f3 o, f3 d, float tmin, float tmax) {
    (interval::contains, quad.hpp:62), spheres do not (interval::surrounds, sphere.hpp:70). So among the
    primitives at the smallest t the last quad of the list wins if there is one, else the first sphere,
    whatever order they are tested in: at equal t a quad replaces a sphere and an earlier quad, a sphere
-   replaces a later sphere (round 5) and no quad. ids are input (list-order) indices. */
+   replaces a later sphere (round 5) and no quad. "Order" is the order the reference tests objects in:
+   a hittable_list's list order, a bvh_node's children left then right (bvh_node.hpp:89-90), i.e. the
+   median tree's leaf order — the descriptor's tie_rank (ABI 7) when present, else the input order. */
+static inline int64_t tie_rank32(const world32* w, int64_t id) {
+  return w->s->abi_version >= 7 && w->s->tie_rank ? w->s->tie_rank[id] : id;
+}
 static int quad_wins_tie32(const world32* w, int64_t id, int64_t best) {
   if (w->s->prims[best].kind != RTG_PRIM_QUAD) return 1;
-  return id > best;
+  return tie_rank32(w, id) > tie_rank32(w, best);
 }
 static int sphere_wins_tie32(const world32* w, int64_t id, int64_t best) {
-  return best >= 0 && w->s->prims[best].kind == RTG_PRIM_SPHERE && id < best;
+  return best >= 0 && w->s->prims[best].kind == RTG_PRIM_SPHERE && tie_rank32(w, id) < tie_rank32(w, best);
 }
 
 /* closest hit: reference BVH order; boxes tested in f64 (pure culling), primitives in fp32 */
@@ -1232,17 +1237,20 @@ int orc_render_f32_mt(const rtg_scene_desc* s, const rtg_camera_desc* cam, uint6
   if (threads > row_count) threads = row_count > 0 ? row_count : 1;
   rows32_arg* args = (rows32_arg*)calloc(threads, sizeof(rows32_arg));
   pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * threads);
+  int* started = (int*)calloc(threads, sizeof(int));
   for (int k = 0; k < threads; ++k) {
     rows32_arg a = {&w, cam, cf, &cp, seed, row_begin, row_stride, row_count, k, threads, out, 0};
     args[k] = a;
-    if (k > 0) pthread_create(&th[k], 0, render_rows32, &args[k]);
+    if (k > 0) started[k] = pthread_create(&th[k], 0, render_rows32, &args[k]) == 0;
   }
   render_rows32(&args[0]);
   uint64_t segs = args[0].segs;
   for (int k = 1; k < threads; ++k) {
-    pthread_join(th[k], 0);
+    if (started[k]) pthread_join(th[k], 0);
+    else render_rows32(&args[k]); /* no thread (e.g. a cgroup thread limit): its rows on this one */
     segs += args[k].segs;
   }
+  free(started);
   if (segments) *segments = segs;
   free(th);
   free(args);
@@ -1402,4 +1410,30 @@ int64_t orc_bvh_replay(const rtg_scene_desc* s, const double o[3], const double 
   *t_hit = h ? rec.t : -1.0;
   world64_free(&w);
   return lg.n;
+}
+
+/* cpu_ref32's closest hit for n rays (o, d, time as fp32, the camera segment's form: tmin 0.001, no
+ * origin primitive): best[k] = the winning primitive (input index, -1 on a miss), t[k] its fp32 t. The
+ * exact-t tie rule decides equal t by the descriptor's tie_rank (tests/test_oracle_golden.py pins it
+ * against the winners of the reference's own compiled hittable_list / bvh_node / sphere / quad). */
+void orc_closest_hit32(const rtg_scene_desc* s, int64_t n, const float* o, const float* d, const float* time,
+                       int64_t* best, float* t) {
+  world32 w;
+  world32_init(&w, s);
+  double bound = 0.0;
+  for (int64_t k = 0; k < n; ++k)
+    for (int a = 0; a < 3; ++a) bound = fmax(bound, fabs((double)o[k * 3 + a]));
+  world32_pad(&w, bound);
+  for (int64_t k = 0; k < n; ++k) {
+    f3 O3 = F3(o[k * 3], o[k * 3 + 1], o[k * 3 + 2]), D3v = F3(d[k * 3], d[k * 3 + 1], d[k * 3 + 2]);
+    float tb = INFINITY;
+    int64_t b = -1;
+    if (w.bvh.n > 0) {
+      const double O[3] = {O3.x, O3.y, O3.z}, Dd[3] = {D3v.x, D3v.y, D3v.z};
+      node_hit32(&w, 0, O3, D3v, O, Dd, time[k], -1, &tb, &b);
+    }
+    best[k] = b;
+    t[k] = b >= 0 ? tb : -1.0f;
+  }
+  world32_free(&w);
 }

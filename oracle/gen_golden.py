@@ -15,6 +15,8 @@ Writes
   tests/golden/reference_scene_g500.json  G1': bouncing_spheres at grid half-width 500 (BASELINE
                                       config 5, 1,000,001 records): per-material counts and the
                                       sha256 of the reference's (N, 13) float64 record array
+  tests/golden/ties.json              exact-t tie winners of the reference's own hittable_list and
+                                      bvh_node over the tie world (scenes.hpp tie_world), 101 rays
   tests/golden/earthmap.ppm           earthmap.jpg decoded to 8-bit sRGB (PIL), the input the image
                                       loader expects in place of stb_image (parity unpinned at the
                                       JPEG decoder: stb vs libjpeg may differ by 1 LSB)
@@ -87,6 +89,15 @@ def gen_moments(only=None) -> None:
         print(f"moments_{scene}: {mean.shape} n={n} segments/sample={segs / (n * W * meta['height']):.4f}")
 
 
+def gen_ties() -> None:
+    out = subprocess.run([HARNESS, "ties"], check=True, capture_output=True, text=True).stdout
+    data = json.loads(out)
+    with open(os.path.join(GOLDEN, "ties.json"), "w") as f:
+        json.dump(data, f, separators=(",", ":"))
+    diff = sum(a != b for a, b in zip(data["list"]["winner"], data["bvh"]["winner"]))
+    print(f"ties.json: {len(data['rays'])} rays, list vs bvh_node winners differ on {diff}")
+
+
 def gen_scene_records() -> None:
     rec = {}
     for grid in (11, 500):
@@ -116,6 +127,7 @@ def main() -> int:
     print("reference_golden.json:", {k: len(v) if isinstance(v, list) else "…" for k, v in data.items()})
 
     gen_hybrid()
+    gen_ties()
     gen_scene_records()
     gen_moments()
 
@@ -153,6 +165,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "hybrid":
         gen_hybrid(sys.argv[2:] or None)
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "ties":
+        gen_ties()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "records":
         gen_scene_records()

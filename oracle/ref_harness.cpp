@@ -15,6 +15,7 @@
 //
 // Modes:
 //   ref_harness golden                     -> JSON golden vectors on stdout
+//   ref_harness ties                       -> exact-t tie winners, plain list vs bvh_node (JSON)
 //   ref_harness render SCENE W H SPP DEPTH SEED OUT.bin   -> fp64 framebuffer + segment count
 //   ref_harness bench SCENE W H SPP DEPTH PROCS [ROWSTEP] -> multi-process timing (JSON)
 //   ref_harness moments SCENE W H SPP DEPTH PROCS SEED0 OUT.bin -> per-pixel sum L, sum L^2 (G5)
@@ -25,6 +26,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -930,8 +932,139 @@ static int records_mode(int grid, const char* outpath) {
   return 0;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// ties: the winner of exactly equal-t hits through the reference's own hittable_list, bvh_node,
+// sphere and quad. The world holds groups of identical spheres, static spheres
+// with a moving twin that coincides at time 0, coplanar quads of different extents and two compound
+// children (hittable_lists of two quads) in the same plane, plus background spheres; every object has
+// its own material, so rec.mat names the winner. Rays leave (0, 0, 30) at time 0 (and a few at 0.37)
+// toward the tie regions. It is rendered as a plain hittable_list ("list": the list rule) and as
+// hittable_list(bvh_node(list)) as main.cpp:76 wraps book-1 ("bvh": the median tree's leaf order).
+// scenes/scenes.hpp tie_world builds the same objects with the C++ mirror; tests/golden/ties.json pins
+// the oracle's tie rule (with the mirror's tie ranks) to these winners.
+struct tie_obj {
+  int kind;  // 1 sphere, 2 quad
+  point3 c0, c1;
+  double r;
+  point3 Q;
+  vec3 u, v;
+};
+static int ties_mode() {
+  std::vector<tie_obj> prims;                       // flattened, list order
+  std::vector<std::shared_ptr<material>> mats;      // one per primitive
+  hittable_list objs;                               // the top-level children
+  std::vector<int> child_prims;                     // primitives per child
+  auto mat = [&]() {
+    const double k = static_cast<double>(mats.size());
+    mats.push_back(std::make_shared<diffuse_light>(color(0.1 + 0.02 * k, 1.0 - 0.02 * k, 0.5)));
+    return mats.back();
+  };
+  auto sph = [&](point3 c0, point3 c1, double r) -> std::shared_ptr<hittable> {
+    prims.push_back(tie_obj{1, c0, c1, r, point3(), vec3(), vec3()});
+    if (c0.x() == c1.x() && c0.y() == c1.y() && c0.z() == c1.z()) return std::make_shared<sphere>(c0, r, mat());
+    return std::make_shared<sphere>(c0, c1, r, mat());
+  };
+  auto qd = [&](point3 Q, vec3 u, vec3 v) -> std::shared_ptr<hittable> {
+    prims.push_back(tie_obj{2, point3(), point3(), 0.0, Q, u, v});
+    return std::make_shared<quad>(Q, u, v, mat());
+  };
+  for (int m = 0; m < 4; ++m)  // 4 groups of 4 identical spheres, the list interleaving the groups
+    for (int g = 0; g < 4; ++g) {
+      const point3 c(-9.0 + 6.0 * g, 4.0, 0.0);
+      objs.add(sph(c, c, 1.5));
+      child_prims.push_back(1);
+    }
+  for (int g = 0; g < 4; ++g) {  // a static sphere, then its moving twin (centre at time 0 the same)
+    const point3 c(-9.0 + 6.0 * g, -4.0, 0.0);
+    objs.add(sph(c, c, 1.5));
+    objs.add(sph(c, c + vec3(g % 2 ? 3.0 : -3.0, 0.0, 0.0), 1.5));
+    child_prims.push_back(1);
+    child_prims.push_back(1);
+  }
+  for (int k = 0; k < 4; ++k) {  // coplanar quads in z = 3, box minima x = -2, -4, -6, -8
+    objs.add(qd(point3(-2.0 - 2.0 * k, -1.0, 3.0), vec3(4.0 + 4.0 * k, 0.0, 0.0), vec3(0.0, 2.0, 0.0)));
+    child_prims.push_back(1);
+  }
+  for (int j = 0; j < 2; ++j) {  // two identical compound children, in the same plane
+    auto pane = std::make_shared<hittable_list>();
+    pane->add(qd(point3(5.0, -1.0, 3.0), vec3(4.0, 0.0, 0.0), vec3(0.0, 2.0, 0.0)));
+    pane->add(qd(point3(5.0, -1.0, 3.0), vec3(2.0, 0.0, 0.0), vec3(0.0, 1.0, 0.0)));
+    objs.add(pane);
+    child_prims.push_back(2);
+  }
+  for (int k = 0; k < 8; ++k) {  // background
+    const point3 c(-14.0 + 4.0 * k, k % 2 ? -8.0 : 8.0, -6.0);
+    objs.add(sph(c, c, 1.0));
+    child_prims.push_back(1);
+  }
+  // rays
+  std::vector<ray> rays;
+  const point3 o(0.0, 0.0, 30.0);
+  auto toward = [&](double x, double y, double z, double t) { rays.push_back(ray(o, point3(x, y, z) - o, t)); };
+  for (int row = 0; row < 2; ++row)
+    for (int g = 0; g < 4; ++g)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) toward(-9.0 + 6.0 * g + 0.5 * dx, (row ? -4.0 : 4.0) + 0.5 * dy, 0.0, 0.0);
+  for (int g = 0; g < 4; ++g) toward(-9.0 + 6.0 * g + 0.25, -4.0 + 0.25, 0.0, 0.375);
+  const double qx[] = {-7.5, -5.5, -3.5, -1.5, 0.0, 1.5, 3.5, 5.25, 5.5, 6.5, 7.5, 8.5};
+  for (double x : qx)
+    for (double y : {-0.5, 0.25}) toward(x, y, 3.0, 0.0);
+  toward(0.0, 20.0, 0.0, 0.0);  // a miss
+  hittable_list plain = objs;
+  hittable_list tree(std::make_shared<bvh_node>(objs));
+  std::map<const material*, int> who;
+  for (size_t i = 0; i < mats.size(); ++i) who[mats[i].get()] = static_cast<int>(i);
+  printf("{\"objects\": [");
+  for (size_t i = 0; i < prims.size(); ++i) {
+    const tie_obj& p = prims[i];
+    printf("%s{", i ? ", " : "");
+    if (p.kind == 1) {
+      printf("\"kind\": \"sphere\", ");
+      pv("c0", p.c0);
+      pv("c1", p.c1);
+      pj("r", p.r, false);
+    } else {
+      printf("\"kind\": \"quad\", ");
+      pv("Q", p.Q);
+      pv("u", p.u);
+      pv("v", p.v, false);
+    }
+    printf("}");
+  }
+  printf("], \"child_prims\": [");
+  for (size_t i = 0; i < child_prims.size(); ++i) printf("%s%d", i ? ", " : "", child_prims[i]);
+  printf("], \"rays\": [");
+  for (size_t k = 0; k < rays.size(); ++k) {
+    printf("%s{", k ? ", " : "");
+    pv("o", rays[k].origin());
+    pv("d", rays[k].direction());
+    pj("time", rays[k].time(), false);
+    printf("}");
+  }
+  printf("]");
+  const hittable* worlds[2] = {&plain, &tree};
+  const char* names[2] = {"list", "bvh"};
+  for (int w = 0; w < 2; ++w) {
+    printf(", \"%s\": {\"winner\": [", names[w]);
+    std::vector<double> ts;
+    for (size_t k = 0; k < rays.size(); ++k) {
+      hit_record rec;
+      const bool h = worlds[w]->hit(rays[k], interval(0.001, infinity), rec);  // camera.hpp:192
+      printf("%s%d", k ? ", " : "", h ? who.at(rec.mat.get()) : -1);
+      ts.push_back(h ? rec.t : -1.0);
+    }
+    printf("], \"t\": ");
+    pa(ts.data(), static_cast<int>(ts.size()));
+    printf("}");
+  }
+  printf("}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc >= 2 && std::string(argv[1]) == "golden") return golden();
+  if (argc >= 2 && std::string(argv[1]) == "ties") return ties_mode();
   if (argc >= 10 && std::string(argv[1]) == "moments")
     return moments_mode(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]), atoi(argv[7]),
                         (unsigned)strtoul(argv[8], nullptr, 10), argv[9]);

@@ -468,6 +468,23 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
       return false;
     }
   }
+  // tie ranks (ABI 7): a permutation of the primitive indices, or none (list order)
+  if (d->tie_rank) {
+    if (d->num_prims > INT32_MAX) {
+      *err = "tie_rank needs fewer than 2^31 primitives";
+      return false;
+    }
+    std::vector<uint8_t> seen(static_cast<size_t>(d->num_prims), 0);
+    for (int64_t i = 0; i < d->num_prims; ++i) {
+      const int64_t r = d->tie_rank[i];
+      if (r < 0 || r >= d->num_prims || seen[r]) {
+        *err = "tie_rank is not a permutation of the primitive indices (index " + std::to_string(i) + ")";
+        return false;
+      }
+      seen[r] = 1;
+    }
+  }
+  auto tie_rank = [d](int64_t i) -> int64_t { return d->tie_rank ? d->tie_rank[i] : i; };
   // M of the culling margin (culling_box): the largest |coordinate| of any primitive box, i.e. of any hit
   // point a later segment starts from; rtg_render widens the boxes when a camera lies farther out
   {
@@ -626,8 +643,8 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         out->spheres.insert(out->spheres.end(), rec, rec + 8);
       } else {
         slot[pid] = nquad++;
-        // quad ctor (quad.hpp:12-27) in fp64, then rounded; the v row's 4th word holds the quad's list
-        // index (the exact-t tie rule's rank, read with the inside test's loads)
+        // quad ctor (quad.hpp:12-27) in fp64, then rounded; the v row's 4th word holds the quad's tie
+        // rank (its position in the reference's test order, read with the inside test's loads)
         const D3 Q = d3(p.p0), u = d3(p.p1), v = d3(p.p2);
         const D3 n = cross(u, v);
         const D3 normal = unit_vector(n);
@@ -638,7 +655,7 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
                                static_cast<float>(u.x),      static_cast<float>(u.y),
                                static_cast<float>(u.z),      ibits_to_float(p.material),
                                static_cast<float>(v.x),      static_cast<float>(v.y),
-                               static_cast<float>(v.z),      ibits_to_float(static_cast<int32_t>(pid)),
+                               static_cast<float>(v.z),      ibits_to_float(static_cast<int32_t>(tie_rank(pid))),
                                static_cast<float>(w.x),      static_cast<float>(w.y),
                                static_cast<float>(w.z),      0.0f,
                                static_cast<float>(normal.x), static_cast<float>(normal.y),
@@ -659,11 +676,11 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
     out->spheres.insert(out->spheres.end(), rec, rec + 8);
   }
 
-  // the exact-t tie rule's list order: input index per sphere slot, then per quad slot
+  // the exact-t tie rule's order: tie rank per sphere slot, then per quad slot
   out->tie_rank.assign(static_cast<size_t>(nsph) + nquad, -1);
   for (int64_t i = 0; i < d->num_prims; ++i)
     if (slot[i] >= 0)
-      out->tie_rank[(d->prims[i].kind == RTG_PRIM_QUAD ? nsph : 0) + slot[i]] = static_cast<int32_t>(i);
+      out->tie_rank[(d->prims[i].kind == RTG_PRIM_QUAD ? nsph : 0) + slot[i]] = static_cast<int32_t>(tie_rank(i));
   phase("prims");
   // culling boxes (the margin above) in place of the reference's, then rounded outward
   if (out->node_width == 4) refit_culling_boxes<BuildNode4, 4>(bvh4.nodes, bvh.refs, d, out->origin_bound);
@@ -927,12 +944,27 @@ rtg_status rtg_bvh_build_host(const rtg_scene_desc* desc, rtg_bvh_node_host* nod
   return RTG_OK;
 }
 
-rtg_status rtg_scene_create(const rtg_scene_desc* desc, int32_t device, rtg_scene** out) {
-  if (!desc || !out) return fail(RTG_E_INVALID, "null argument");
+rtg_status rtg_bvh_node_order(const double* boxes, int64_t n, int64_t* order) {
+  if (n < 0 || (n > 0 && (!boxes || !order))) return fail(RTG_E_INVALID, "null array or negative count");
+  try {
+    bvh_node_order(boxes, n, order);
+  } catch (const std::bad_alloc&) {
+    return fail(RTG_E_NOMEM, "rtg_bvh_node_order: out of host memory");
+  }
+  return RTG_OK;
+}
+
+rtg_status rtg_scene_create(const rtg_scene_desc* desc_in, int32_t device, rtg_scene** out) {
+  if (!desc_in || !out) return fail(RTG_E_INVALID, "null argument");
   *out = nullptr;
-  if (desc->abi_version != RTG_ABI_VERSION)
+  if (desc_in->abi_version != RTG_ABI_VERSION && desc_in->abi_version != 6)
     return fail(RTG_E_INVALID, "abi_version mismatch (expected " +
-                                   std::to_string(RTG_ABI_VERSION) + ")");
+                                   std::to_string(RTG_ABI_VERSION) + " or 6)");
+  // an ABI-6 descriptor ends before tie_rank: read only its own bytes
+  rtg_scene_desc desc_v{};
+  std::memcpy(&desc_v, desc_in,
+              desc_in->abi_version == 6 ? offsetof(rtg_scene_desc, tie_rank) : sizeof(rtg_scene_desc));
+  const rtg_scene_desc* desc = &desc_v;
   // validate + compile first (host only), so malformed scenes report RTG_E_INVALID anywhere
   const auto t0 = std::chrono::steady_clock::now();
   HostScene hs;

@@ -872,6 +872,59 @@ bool hot_order_nodes(int32_t* rec, int width, const uint32_t* visits, int64_t n,
   return true;
 }
 
+// ---- bvh_node's leaf order (rtg_bvh_node_order) ----
+// The permutation bvh_node(objects, 0, n) applies to `objects` (bvh_node.hpp:25-77): a node of three or
+// more objects sorts its range by box min on its box's longest axis and splits it at the median, spans
+// of 1 and 2 stay as they are; the final array is the leaves left to right. The sort is libstdc++'s
+// std::sort as in the reference, run on (key, id) pairs instead of shared_ptrs: the same comparisons in
+// the same sequence, so the same permutation, equal keys included (book-1's root sorts 483 equal y-mins).
+// The two halves of a large range are ordered concurrently (disjoint ranges of ids and scratch).
+namespace {
+struct NodeOrder {
+  struct KeyId {
+    double key;
+    int64_t id;
+  };
+  const Box* boxes;
+  int64_t* ids;
+  KeyId* scratch;
+
+  void run(int64_t start, int64_t end, int spawn) {
+    const int64_t span = end - start;
+    if (span <= 2) return;
+    Box b;
+    for (int64_t i = start; i < end; ++i) b = box_union(b, boxes[ids[i]]);
+    const int axis = longest_axis(b);
+    KeyId* kv = scratch + start;
+    for (int64_t k = 0; k < span; ++k) kv[k] = KeyId{boxes[ids[start + k]].lo[axis], ids[start + k]};
+    std::sort(kv, kv + span, [](const KeyId& x, const KeyId& y) { return x.key < y.key; });
+    for (int64_t k = 0; k < span; ++k) ids[start + k] = kv[k].id;
+    const int64_t mid = start + span / 2;
+    if (spawn > 0 && span >= 32768) {
+      std::thread left([this, start, mid, spawn]() { run(start, mid, spawn - 1); });
+      run(mid, end, spawn - 1);
+      left.join();
+    } else {
+      run(start, mid, 0);
+      run(mid, end, 0);
+    }
+  }
+};
+}  // namespace
+
+void bvh_node_order(const double* boxes6, int64_t n, int64_t* order) {
+  std::vector<Box> boxes(n);
+  for (int64_t i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a) {
+      boxes[i].lo[a] = boxes6[i * 6 + a];
+      boxes[i].hi[a] = boxes6[i * 6 + 3 + a];
+    }
+  for (int64_t i = 0; i < n; ++i) order[i] = i;
+  std::vector<NodeOrder::KeyId> scratch(n);
+  NodeOrder o{boxes.data(), order, scratch.data()};
+  o.run(0, n, 4);  // up to 16 concurrent subtrees (the GPU box's 16-core quota)
+}
+
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err) {
   out->nodes.clear();
   out->refs.clear();

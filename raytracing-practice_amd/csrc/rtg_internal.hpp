@@ -123,6 +123,8 @@ constexpr int node_bytes(int width) { return 28 * width; }
 void prim_bbox(const rtg_primitive& p, double lo[3], double hi[3]);
 
 bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err);
+// rtg_bvh_node_order: the leaf order of bvh_node(objects, 0, n) over n boxes {lo.xyz, hi.xyz} (rtg_bvh.cpp)
+void bvh_node_order(const double* boxes6, int64_t n, int64_t* order);
 bool compile_scene(const rtg_scene_desc* desc, HostScene* out, std::string* err);
 void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* out);
 // rtg_last_error() text of the calling thread; returns `code` (rtg_api.cpp)

@@ -3,11 +3,16 @@
 // On the device the library builds its own BVH over the flattened primitives (RTG_BVH_MEDIAN
 // reproduces this topology, RTG_BVH_SAH is the fast default); flattening a bvh_node therefore
 // emits the objects in the order of the list it was built from (the root keeps that order), so
-// the flat scene lists objects exactly as the reference's hittable_list did.
+// the flat scene lists objects exactly as the reference's hittable_list did, and records the order
+// the reference's bvh_node::hit tests them in — its leaves left to right (rtg_bvh_node_order) — as
+// the primitives' tie ranks (rtg_scene_desc.tie_rank): at an exactly equal t the reference keeps the
+// first sphere and the last quad of THAT order (bvh_node.hpp:89-90, sphere.hpp:70, quad.hpp:62).
 #pragma once
 #include <algorithm>
 #include <atomic>
 #include <mutex>
+#include <string>
+#include <vector>
 
 #include "accelerator/aabb.hpp"
 #include "hittable/hittable.hpp"
@@ -78,9 +83,37 @@ class bvh_node : public hittable {
 
   bool rtg_flatten(rtgpu::scene_builder& sb, const vec3& offset) const override {
     if (!list_order.empty()) {
-      sb.reserve(list_order.size());
-      for (const auto& obj : list_order)
-        if (!obj->rtg_flatten(sb, offset)) return false;
+      const size_t n = list_order.size();
+      sb.reserve(n);
+      std::vector<size_t> first(n + 1);  // child k's primitives: [first[k], first[k + 1])
+      std::vector<double> boxes(6 * n);  // child k's bounding_box(), the key the reference sorts by
+      for (size_t k = 0; k < n; ++k) {
+        first[k] = sb.prims.size();
+        if (!list_order[k]->rtg_flatten(sb, offset)) return false;
+        const aabb b = list_order[k]->bounding_box();
+        for (int a = 0; a < 3; ++a) {
+          boxes[6 * k + a] = b.axis_interval(a).min;
+          boxes[6 * k + 3 + a] = b.axis_interval(a).max;
+        }
+      }
+      first[n] = sb.prims.size();
+      std::vector<int64_t> order(n);
+      if (rtg_bvh_node_order(boxes.data(), static_cast<int64_t>(n), order.data()) != RTG_OK)
+        return sb.fail(std::string("rtg_bvh_node_order: ") + rtg_last_error());
+      bool identity = true;
+      for (size_t k = 0; k < n && identity; ++k) identity = order[k] == static_cast<int64_t>(k);
+      if (identity) return true;
+      // the range's ranks: the children in leaf order, each child keeping its own primitives' order
+      // (child k's ranks are a permutation of [first[k], first[k + 1]), identity unless it reordered them)
+      sb.extend_ranks(first[n]);
+      const std::vector<int64_t> own(sb.tie_rank.begin() + first[0], sb.tie_rank.begin() + first[n]);
+      int64_t base = static_cast<int64_t>(first[0]);
+      for (size_t pos = 0; pos < n; ++pos) {
+        const size_t c = static_cast<size_t>(order[pos]);
+        for (size_t i = first[c]; i < first[c + 1]; ++i)
+          sb.tie_rank[i] = base + (own[i - first[0]] - static_cast<int64_t>(first[c]));
+        base += static_cast<int64_t>(first[c + 1] - first[c]);
+      }
       return true;
     }
     if (!left) return true;  // built over an empty list: nothing to flatten

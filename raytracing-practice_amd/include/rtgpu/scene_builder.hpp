@@ -24,7 +24,17 @@ class scene_builder {
   std::vector<rtg_image> images;
   std::vector<std::shared_ptr<const std::vector<uint8_t>>> image_bytes;
   std::vector<rtg_perlin> perlins;
+  // Exact-t tie order (rtg_scene_desc.tie_rank, ABI 7): per primitive its position in the order the
+  // reference's closest-hit walk tests it. Empty while that is the primitive order (hittable_list order);
+  // a bvh_node's flatten permutes its own range into its median tree's leaf order (bvh_node.hpp:80-94).
+  std::vector<int64_t> tie_rank;
   std::string error;
+
+  // identity ranks for the primitives [tie_rank.size(), n) (before a bvh_node permutes a range)
+  void extend_ranks(size_t n) {
+    tie_rank.reserve(n);
+    for (size_t i = tie_rank.size(); i < n; ++i) tie_rank.push_back(static_cast<int64_t>(i));
+  }
 
   // Index of the flattened material / texture (exports on first use); -1 on failure.
   int32_t material_id(const material* m);  // defined in core/material.hpp
@@ -64,7 +74,8 @@ class scene_builder {
   // identity -> index table, one per exported object kind (hashed: config 5 flattens 1M materials)
   std::unordered_map<const void*, int32_t>& memo_table(memo_kind k) { return memo_[k]; }
 
-  rtg_scene_desc desc(int32_t bvh_mode) const {
+  rtg_scene_desc desc(int32_t bvh_mode) {
+    if (!tie_rank.empty()) extend_ranks(prims.size());
     rtg_scene_desc d{};
     d.abi_version = RTG_ABI_VERSION;
     d.bvh_mode = bvh_mode;
@@ -78,6 +89,7 @@ class scene_builder {
     d.num_images = static_cast<int32_t>(images.size());
     d.perlins = perlins.data();
     d.num_perlins = static_cast<int32_t>(perlins.size());
+    d.tie_rank = tie_rank.empty() ? nullptr : tie_rank.data();
     return d;
   }
 

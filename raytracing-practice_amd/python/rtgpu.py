@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 
-RTG_ABI_VERSION = 6
+RTG_ABI_VERSION = 7
 RTG_OK = 0
 RTG_E_INVALID, RTG_E_HIP, RTG_E_NODEVICE, RTG_E_NOMEM, RTG_E_UNSUPPORTED = -1, -2, -3, -4, -5
 RTG_PRIM_SPHERE, RTG_PRIM_QUAD = 1, 2
@@ -75,7 +75,8 @@ class rtg_scene_desc(C.Structure):
                 ("materials", C.POINTER(rtg_material)), ("num_materials", C.c_int32),
                 ("num_textures", C.c_int32), ("textures", C.POINTER(rtg_texture)),
                 ("images", C.POINTER(rtg_image)), ("num_images", C.c_int32),
-                ("num_perlins", C.c_int32), ("perlins", C.POINTER(rtg_perlin))]
+                ("num_perlins", C.c_int32), ("perlins", C.POINTER(rtg_perlin)),
+                ("tie_rank", C.POINTER(C.c_int64))]  # ABI 7: the reference's test order (NULL: list order)
 
 
 class rtg_camera_desc(C.Structure):
@@ -143,7 +144,7 @@ RTG_SYMBOLS = ("rtg_abi_version", "rtg_last_error", "rtg_device_count", "rtg_cam
                "rtg_comm_unique_id", "rtg_comm_create_rank", "rtg_comm_size", "rtg_comm_destroy",
                "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame", "rtg_render_plan",
                "rtg_shard_layout", "rtg_deinterleave_rows_host", "rtg_scene_prepare",
-               "rtg_hot_treelet_order_host")
+               "rtg_hot_treelet_order_host", "rtg_bvh_node_order")
 RTG_COMM_ID_BYTES = 128
 
 
@@ -226,11 +227,13 @@ class Library:
         L.rtg_hot_treelet_order_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.rtg_shard_layout.argtypes = [C.c_int32, C.c_int32, C.c_int32] + [_P(C.c_int32)] * 4
         L.rtg_deinterleave_rows_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64]
+        L.rtg_bvh_node_order.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
         for name in ("rtg_device_count", "rtg_camera_resolve", "rtg_scene_create",
                      "rtg_scene_get_info", "rtg_render", "rtg_render_wait", "rtg_resolve_rgb8",
                      "rtg_bvh_build_host", "rtg_comm_create_local", "rtg_comm_unique_id",
                      "rtg_comm_create_rank", "rtg_comm_size", "rtg_gather_rows", "rtg_deinterleave_rows",
-                     "rtg_render_frame", "rtg_render_plan", "rtg_shard_layout", "rtg_deinterleave_rows_host"):
+                     "rtg_render_frame", "rtg_render_plan", "rtg_shard_layout", "rtg_deinterleave_rows_host",
+                     "rtg_bvh_node_order"):
             getattr(L, name).restype = C.c_int32
         if L.rtg_abi_version() != RTG_ABI_VERSION:
             raise RuntimeError("librtgpu ABI version mismatch")
@@ -259,6 +262,16 @@ class Library:
         self.check("rtg_bvh_build_host", self.lib.rtg_bvh_build_host(
             C.byref(desc), nodes, nn.value, refs, nr.value, C.byref(nn), C.byref(nr), C.byref(depth)))
         return list(nodes)[:nn.value], list(refs)[:nr.value], depth.value
+
+    def bvh_node_order(self, boxes):
+        """rtg_bvh_node_order: list indices in bvh_node(objects, 0, n)'s leaf order, for n object boxes
+        given as an (n, 6) array {lo.xyz, hi.xyz} in list order (bvh_node.hpp:25-77; host only)."""
+        import numpy as np
+
+        b = np.ascontiguousarray(boxes, dtype=np.float64).reshape(-1, 6)
+        out = np.empty(len(b), dtype=np.int64)
+        self.check("rtg_bvh_node_order", self.lib.rtg_bvh_node_order(b.ctypes.data, len(b), out.ctypes.data))
+        return out
 
     def scene_create(self, desc: rtg_scene_desc, device: int = 0) -> "DeviceScene":
         h = C.c_void_p()

@@ -219,6 +219,49 @@ inline scene earth_perlin() {
   return s;
 }
 
+// Exact-t ties inside a bvh_node (not in main.cpp): groups of identical spheres,
+// static spheres with a moving twin that coincides at time 0, coplanar quads of different extents and
+// two identical compound children (hittable_lists of two quads) in the same plane, plus background
+// spheres, every object emitting its own colour (so a pixel shows which object won). oracle/ref_harness.cpp
+// "ties" builds the same objects with the reference's own classes and records the winners of exactly
+// equal t, as a plain list and wrapped in bvh_node as main.cpp:76 wraps book-1 (tests/golden/ties.json).
+// as_list = false: hittable_list(bvh_node(objects)), whose ties follow the median tree's leaf order.
+inline scene tie_world(bool as_list = false) {
+  hittable_list objs;
+  int k = 0;
+  auto mat = [&k]() {
+    const double c = static_cast<double>(k++);
+    return std::make_shared<diffuse_light>(color(0.1 + 0.02 * c, 1.0 - 0.02 * c, 0.5));
+  };
+  for (int m = 0; m < 4; ++m)  // 4 groups of 4 identical spheres, the list interleaving the groups
+    for (int g = 0; g < 4; ++g) objs.add(std::make_shared<sphere>(point3(-9.0 + 6.0 * g, 4.0, 0.0), 1.5, mat()));
+  for (int g = 0; g < 4; ++g) {  // a static sphere, then its moving twin (the same centre at time 0)
+    const point3 c(-9.0 + 6.0 * g, -4.0, 0.0);
+    objs.add(std::make_shared<sphere>(c, 1.5, mat()));
+    objs.add(std::make_shared<sphere>(c, c + vec3(g % 2 ? 3.0 : -3.0, 0.0, 0.0), 1.5, mat()));
+  }
+  for (int q = 0; q < 4; ++q)  // coplanar quads in z = 3, box minima x = -2, -4, -6, -8
+    objs.add(std::make_shared<quad>(point3(-2.0 - 2.0 * q, -1.0, 3.0), vec3(4.0 + 4.0 * q, 0.0, 0.0),
+                                    vec3(0.0, 2.0, 0.0), mat()));
+  for (int j = 0; j < 2; ++j) {  // two identical compound children in the same plane
+    auto pane = std::make_shared<hittable_list>();
+    pane->add(std::make_shared<quad>(point3(5.0, -1.0, 3.0), vec3(4.0, 0.0, 0.0), vec3(0.0, 2.0, 0.0), mat()));
+    pane->add(std::make_shared<quad>(point3(5.0, -1.0, 3.0), vec3(2.0, 0.0, 0.0), vec3(0.0, 1.0, 0.0), mat()));
+    objs.add(pane);
+  }
+  for (int b = 0; b < 8; ++b)  // background
+    objs.add(std::make_shared<sphere>(point3(-14.0 + 4.0 * b, b % 2 ? -8.0 : 8.0, -6.0), 1.0, mat()));
+  scene s{as_list ? std::make_shared<hittable_list>(objs)
+                  : std::make_shared<hittable_list>(std::make_shared<bvh_node>(objs)),
+          camera()};
+  s.cam.image_width = 96;
+  s.cam.aspect_ratio = 1.5;
+  s.cam.samples_per_pixel = 4;
+  s.cam.max_depth = 3;
+  sky_camera(s.cam, 44.0, point3(0.0, 0.0, 30.0), point3(0.0, 0.0, 0.0), color(0.0, 0.0, 0.0));
+  return s;
+}
+
 inline const std::map<std::string, std::function<scene(int)>>& registry() {
   static const std::map<std::string, std::function<scene(int)>> r = {
       {"bouncing_spheres", [](int g) { return bouncing_spheres(g > 0 ? g : 11); }},
@@ -230,6 +273,7 @@ inline const std::map<std::string, std::function<scene(int)>>& registry() {
       {"cornell_box", [](int) { return cornell_box(); }},
       {"cornell_translate", [](int) { return cornell_translate(); }},
       {"earth_perlin", [](int) { return earth_perlin(); }},
+      {"tie_world", [](int g) { return tie_world(g == 1); }},  // grid 1: the plain list
   };
   return r;
 }

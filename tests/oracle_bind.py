@@ -49,6 +49,9 @@ class Oracle:
         L.orc_bvh_replay.argtypes = [P(rtgpu.rtg_scene_desc), D3P, D3P, C.c_double, P(C.c_int64),
                                      C.c_int64, D3P]
         L.orc_bvh_replay.restype = C.c_int64
+        L.orc_closest_hit32.argtypes = [P(rtgpu.rtg_scene_desc), C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p]
+        L.orc_closest_hit32.restype = None
         L.orc_sincos_turn.argtypes = [C.c_float, P(C.c_float), P(C.c_float)]
         for name, nargs in (("orc_sin_spec", 1), ("orc_atan2_spec", 2), ("orc_acos_spec", 1)):
             getattr(L, name).argtypes = [C.c_float] * nargs
@@ -164,6 +167,19 @@ class Oracle:
 
     def perlin_turb(self, perlin, p):
         return self.lib.orc_perlin_turb64(C.byref(perlin), self._d(p))
+
+    def closest_hit32(self, desc, o, d, time):
+        """cpu_ref32's closest hit of n camera-like segments (fp32 rays): (winner index or -1, t)."""
+        import numpy as np
+
+        o = np.ascontiguousarray(o, dtype=np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(d, dtype=np.float32).reshape(-1, 3)
+        tm = np.ascontiguousarray(np.broadcast_to(np.asarray(time, np.float32), (len(o),)))
+        best = np.empty(len(o), np.int64)
+        t = np.empty(len(o), np.float32)
+        self.lib.orc_closest_hit32(C.byref(desc), len(o), o.ctypes.data, d.ctypes.data, tm.ctypes.data,
+                                   best.ctypes.data, t.ctypes.data)
+        return best, t
 
     def bvh_replay(self, desc, o, d, time, cap=4096):
         log, t = (C.c_int64 * cap)(), (C.c_double * 1)()

@@ -647,6 +647,31 @@ def test_sphere_ties_follow_list_order(gpu_lib, oracle, bvh):
     assert np.array_equal(g, g1)
 
 
+@pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
+def test_bvh_node_world_ties_follow_leaf_order(gpu_lib, scenes, oracle, bvh):
+    """Exact-t ties in a world the reference wraps in a bvh_node (main.cpp:76): the
+    reference keeps the first sphere and the last quad in its median tree's LEAF order (bvh_node.hpp:89-90),
+    which the C++ mirror's bvh_node hands the library as tie ranks (rtg_scene_desc.tie_rank). tie_world
+    (identical sphere groups, coplanar quads, identical compound children, every object its own colour)
+    rendered wrapped in bvh_node and as a plain list: each frame and segment count is cpu_ref32's bit for
+    bit for every BVH builder (the oracle's rule is pinned to the reference's own winners by
+    test_oracle_golden.py::test_tie_winners_match_reference), and the two frames differ (the ranks reach
+    the kernel)."""
+    frames = {}
+    for grid, key in ((0, "bvh_node"), (1, "list")):
+        s = scenes.build("tie_world", grid=grid, bvh_mode=bvh)
+        assert bool(s.desc.tie_rank) == (key == "bvh_node")
+        cam = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+        ds = gpu_lib.scene_create(s.desc)
+        g, st = ds.render_host(cam)
+        ds.close()
+        o, segs = oracle.render_f32(s.desc, cam)
+        assert np.array_equal(g, o) and st.segments == segs, (key, float(np.mean(np.all(g == o, axis=-1))))
+        frames[key] = g
+    differ = int(np.sum(np.any(frames["bvh_node"] != frames["list"], axis=-1)))
+    assert differ > 500, differ
+
+
 @pytest.mark.parametrize("competitor", ["quad", "sphere"])
 @pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
 def test_near_tie_culling_is_conservative(gpu_lib, oracle, bvh, competitor):

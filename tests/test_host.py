@@ -200,6 +200,56 @@ def test_median_bvh_topology_matches_bvh_node(lib, scenes, oracle, golden):
         assert h == bool(ray["hit"]) and (not h or t == ray["t"])
 
 
+@pytest.mark.parametrize("name,grid", [("bouncing_spheres", 11), ("bouncing_spheres", 40), ("tie_world", 0)])
+def test_tie_ranks_are_the_median_tree_leaf_order(lib, scenes, name, grid):
+    """The C++ mirror's bvh_node hands the order its hit() tests objects in as tie ranks (ABI 7,
+    rtg_scene_desc.tie_rank, from rtg_bvh_node_order): for a world of primitives wrapped in one bvh_node that
+    is the leaf order of the reference's median tree, which RTG_BVH_MEDIAN rebuilds node for node (pinned
+    above), so the primitives sorted by rank are that build's leaf references exactly. Book-1's root sorts
+    483 equal y-minima (std::sort's placement of equal keys matters); tie_world has compound children."""
+    s = scenes.build(name, grid=grid)
+    r = np.ctypeslib.as_array(s.desc.tie_rank, shape=(s.desc.num_prims,))
+    assert sorted(r.tolist()) == list(range(s.desc.num_prims))
+    if name == "tie_world":  # children of two quads: ranks keep each child's two primitives adjacent
+        assert int(r[29]) == int(r[28]) + 1 and int(r[31]) == int(r[30]) + 1
+        return
+    m = scenes.build(name, grid=grid, bvh_mode=rtgpu.RTG_BVH_MEDIAN)
+    _, refs, _ = lib.bvh_build_host(m.desc)
+    assert np.argsort(r).tolist() == list(refs)
+
+
+def test_bvh_node_order_matches_sort_semantics(lib):
+    """rtg_bvh_node_order on hand-made boxes: spans of one and two are not sorted (bvh_node.hpp:53-62),
+    three or more are sorted by box minimum on the longest axis of their box and split at the median."""
+    def box(x, y=0.0, z=0.0, w=1.0):
+        return [x, y, z, x + w, y + w, z + w]
+    assert lib.bvh_node_order([box(5), box(1)]).tolist() == [0, 1]          # two: left, right as listed
+    assert lib.bvh_node_order([box(5), box(1), box(3)]).tolist() == [1, 2, 0]  # three: sorted on x
+    # longest axis y: sorted by y-min whatever the x order
+    assert lib.bvh_node_order([box(0, 9, w=0.5), box(1, 0, w=0.5), box(2, 4, w=0.5)]).tolist() == [1, 2, 0]
+    assert lib.bvh_node_order([]).tolist() == []
+
+
+def test_tie_rank_must_be_a_permutation(lib, scenes):
+    """rtg_scene_create validates tie_rank before any device work (RTG_E_INVALID anywhere); an ABI-6
+    descriptor (no tie_rank field) is still accepted and read as list order (here: no device ->
+    RTG_E_NODEVICE, i.e. it got past validation)."""
+    import ctypes as C
+
+    s = scenes.build("tie_world", grid=0)
+    d = rtgpu.rtg_scene_desc.from_buffer_copy(s.desc)
+    bad = (C.c_int64 * d.num_prims)(*([0] * d.num_prims))
+    d.tie_rank = C.cast(bad, C.POINTER(C.c_int64))
+    with pytest.raises(rtgpu.RtgError) as e:
+        lib.scene_create(d)
+    assert e.value.status == rtgpu.RTG_E_INVALID and "permutation" in str(e.value)
+    if lib.device_count() == 0:
+        d.abi_version = 6  # bytes past the ABI-6 layout (the bad ranks) are not read
+        with pytest.raises(rtgpu.RtgError) as e:
+            lib.scene_create(d)
+        assert e.value.status == rtgpu.RTG_E_NODEVICE
+
+
 @pytest.mark.parametrize("name", ["bouncing_spheres", "cornell_box", "simple_light"])
 def test_sah_bvh_is_complete(lib, scenes, name):
     s = scenes.build(name, rand_seed=1, bvh_mode=rtgpu.RTG_BVH_SAH)

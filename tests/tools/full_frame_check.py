@@ -48,6 +48,18 @@ def main():
     gpu, st = ds.render_host(cam)
     ds.close()
     H = gpu.shape[0]
+    tie_rule = None
+    if s.desc.tie_rank:  # the same frame with list-order ranks: the pixels the bvh_node tie order decides
+        d_list = rtgpu.rtg_scene_desc.from_buffer_copy(s.desc)
+        d_list.tie_rank = None
+        ds = lib.scene_create(d_list)
+        g_list, st_list = ds.render_host(cam)
+        ds.close()
+        dl = np.any(gpu != g_list, axis=-1)
+        yl, xl = np.nonzero(dl)
+        tie_rule = {"pixels_differing_from_list_order": int(dl.sum()),
+                    "segments_list_order": int(st_list.segments),
+                    "where": [[int(x), int(y)] for y, x in zip(yl[:64], xl[:64])]}
     r1 = H if a.rows_to < 0 else min(H, a.rows_to)
     print(f"gpu frame {gpu.shape} in {time.time() - t0:.1f} s, segments {st.segments}", flush=True)
     orc = Oracle()
@@ -72,6 +84,8 @@ def main():
            "gpu_segments_whole_frame": int(st.segments),
            "oracle_seconds": round(time.time() - t0, 1), "threads": a.threads,
            "differing": [[int(x), int(y) + a.rows_from] for y, x in zip(ys[:64], xs[:64])]}
+    if tie_rule is not None:
+        out["tie_rule"] = tie_rule
     if a.rows_from == 0 and r1 == H:
         out["segments_equal"] = int(segs) == int(st.segments)
     print(json.dumps(out, indent=1), flush=True)

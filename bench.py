@@ -19,9 +19,11 @@ time of the K timed steps. Prints ONE JSON line on rank 0.
 Every line carries the per-pixel check of the benchmark frame itself (`parity`: rows of the last timed
 frame — at N > 1 the frame gathered on rank 0 — against the oracle's fp32 spec on the same seeds).
 N > 1 lines also carry `ranks` (each rank's rows, segments, kernel and gather times, all-gathered
-after timing) and `rtg_gather_check`: after the timed loop, the same shards gathered once more through
-the C-ABI's own RCCL gather (rtg_comm_create_rank, ranks_seen from ncclCommCount) and compared byte for
-byte with the timed frame, under a watchdog, so a fault in that path cannot lose the line.
+after timing) and `rtg_gather_check`: after the timed loop, the same shards gathered through the C-ABI's
+own RCCL gather (rtg_comm_create_rank, ranks_seen from ncclCommCount) once per timed step, each call
+timed on the render stream (the product gather's time beside the timed torch gather's, and the library's
+allocations across the calls), the frame compared byte for byte with the timed one, under a watchdog, so a
+fault in that path cannot lose the line.
 """
 import argparse
 import json
@@ -578,7 +580,8 @@ def main():
                 line["parity"]["frame"] = f"gathered on rank 0 from {world} ranks"
 
     if world > 1 and not args.no_rtg_check and not gloo:
-        # the C-ABI's RCCL gather, untimed, on the last frame's shards: byte-compared with the timed frame
+        # the C-ABI's RCCL gather, outside the timed region, on the last frame's shards, once per timed step:
+        # its per-call time beside the timed torch gather's, and byte-compared with the timed frame
         def give_up():
             if rank == 0:
                 line["rtg_gather_check"] = {"status": f"timeout after {args.check_timeout:.0f} s"}
@@ -588,7 +591,7 @@ def main():
         with _Watchdog(args.check_timeout, give_up):
             line_check = rtg_gather_check(lib, dist, torch, world, rank, local, H, W,
                                           shard8 if shard8 is not None else shard,
-                                          gathered[0] if rank == 0 else None, stream)
+                                          gathered[0] if rank == 0 else None, stream, args.steps)
         if rank == 0:
             line["rtg_gather_check"] = line_check
     if rank == 0:
@@ -601,10 +604,13 @@ def main():
         dist.destroy_process_group()
 
 
-def rtg_gather_check(lib, dist, torch, world, rank, local, H, W, src, timed_frame, stream):
-    """One rtg_gather_rows of this rank's last shard (rtg_comm_create_rank; the id broadcast over
-    torch.distributed) into a fresh frame on rank 0, compared byte for byte with the frame the timed
-    loop gathered. Returns the check record on rank 0."""
+def rtg_gather_check(lib, dist, torch, world, rank, local, H, W, src, timed_frame, stream, calls):
+    """The C-ABI's own gather (rtg_gather_rows through rtg_comm_create_rank; the id broadcast over
+    torch.distributed) of this rank's last shard into a fresh frame on rank 0, once per timed step
+    (`calls`), each call timed with an event pair on the render stream like the timed torch gather:
+    the product gather's time beside torch's, and the library's allocation count across the calls (0
+    after the first: the communicator keeps its staging buffer). The frame is compared byte for byte
+    with the one the timed loop gathered. Returns the check record on rank 0."""
     t0 = time.perf_counter()
     uid = [lib.comm_unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
@@ -613,18 +619,26 @@ def rtg_gather_check(lib, dist, torch, world, rank, local, H, W, src, timed_fram
         ranks_seen = comm.size()[0]
         out = torch.zeros((H, W, 3), dtype=src.dtype, device="cuda") if rank == 0 else None
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        comm.gather_rows([src.data_ptr()], H, W * 3 * src.element_size(), 0,
-                         out.data_ptr() if out is not None else 0, [stream])
-        e1.record()
+        calls = max(1, calls)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(calls)]
+        allocs = []
+        for e0, e1 in ev:
+            e0.record()
+            comm.gather_rows([src.data_ptr()], H, W * 3 * src.element_size(), 0,
+                             out.data_ptr() if out is not None else 0, [stream])
+            e1.record()
+            allocs.append(lib.allocation_count()[0])
         torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in ev]
         rec = None
         if rank == 0:
             same = bool(torch.equal(out, timed_frame)) if timed_frame is not None else None
+            later = ms[1:] or ms
             rec = {"status": "ok", "impl": "rtg_gather_rows (ncclGather + de-interleave kernel)",
-                   "ranks_seen": ranks_seen, "identical_to_timed_frame": same,
-                   "gather_ms": round(e0.elapsed_time(e1), 3),
+                   "ranks_seen": ranks_seen, "identical_to_timed_frame": same, "calls": calls,
+                   "gather_ms_first": round(ms[0], 3),
+                   "gather_ms": round(sum(later) / len(later), 3), "gather_ms_max": round(max(later), 3),
+                   "allocations_after_first_call": allocs[-1] - allocs[0],
                    "seconds_incl_comm_init": round(time.perf_counter() - t0, 3)}
         dist.barrier()
         return rec

@@ -384,9 +384,10 @@ rtg_status rtg_shard_layout(int32_t height, int32_t nranks, int32_t rank, int32_
  * rows in image order (ignored by processes without the root). streams[i] (hipStream_t, may be
  * NULL = the communicator's own) orders the gather after the render that filled shards[i].
  * Asynchronous: returns once enqueued (every local rank's part, one RCCL group). The root's staging
- * buffer is allocated per call on its stream (stream-ordered), so gathers in flight on different
- * streams do not share it; calls that use a communicator from several host threads at once are
- * not supported (RCCL groups are per thread). */
+ * buffer belongs to the communicator, grown on demand and kept (ABI 7: steady-state gathers allocate
+ * nothing); a gather on another stream than the previous one first waits for that one's
+ * de-interleave, so gathers in flight on two streams take turns at it. Calls that use a communicator
+ * from several host threads at once are not supported (RCCL groups are per thread). */
 rtg_status rtg_gather_rows(rtg_comm* comm, const void* const* shards, int32_t height, int64_t row_bytes,
                            int32_t root, void* out, void* const* streams);
 
@@ -423,6 +424,12 @@ typedef struct rtg_bvh_node_host {
 rtg_status rtg_bvh_build_host(const rtg_scene_desc* desc, rtg_bvh_node_host* nodes_out,
                               int64_t max_nodes, int64_t* refs_out, int64_t max_refs,
                               int64_t* num_nodes, int64_t* num_refs, int32_t* depth);
+
+/* ABI 7: device and pinned-host allocations librtgpu made in this process so far (count, bytes). Scene
+ * creation allocates; a render, rtg_gather_rows and rtg_render_frame allocate only while their
+ * grow-only buffers (the scene's render scratch and output, the communicator's shards, frame and
+ * staging) reach a frame's sizes, nothing per frame after that. Either pointer may be NULL. */
+rtg_status rtg_allocation_count(uint64_t* count, uint64_t* bytes);
 
 /* Host-only (ABI 7): the order in which bvh_node(objects, 0, n) (bvh_node.hpp:25-77) leaves `objects`
  * — its leaves left to right, the order bvh_node::hit (bvh_node.hpp:80-94) tests them in. boxes holds

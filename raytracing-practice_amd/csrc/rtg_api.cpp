@@ -5,6 +5,7 @@
 // the gfx950 render kernel (rtg_kernels.hip) on the caller's stream. No CPU fallback exists:
 // without a usable device every entry point that renders returns RTG_E_NODEVICE / RTG_E_HIP.
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <functional>
 #include <chrono>
@@ -83,17 +84,13 @@ rtg_status hip_fail(hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(e_, what); \
   } while (0)
 
-// Stream-ordered scratch of one render (stack spill, wave trace, chunk partial sums): freed on
-// the render stream on every exit, the early error returns included, so a failed launch never
-// leaks the (config 5: 6.3 GB) partial-sum buffer.
-struct StreamScratch {
+// A render that returns an error after enqueuing work waits for its stream first, so the scene's scratch
+// (below) is idle again whatever the caller does next.
+struct SyncOnError {
   hipStream_t stream = nullptr;
-  void* ptr[4] = {};
-  int n = 0;
-  void** add() { return &ptr[n++]; }
-  ~StreamScratch() {
-    for (int k = 0; k < n; ++k)
-      if (ptr[k]) (void)hipFreeAsync(ptr[k], stream);  // teardown: nothing to report to
+  bool committed = false;
+  ~SyncOnError() {
+    if (!committed && stream) (void)hipStreamSynchronize(stream);  // error path: the first error is reported
   }
 };
 
@@ -842,7 +839,45 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
   return true;
 }
 
+// Every device / pinned-host allocation of the library goes through these, so rtg_allocation_count can
+// show that steady-state frames allocate nothing.
+std::atomic<uint64_t> g_allocs{0}, g_alloc_bytes{0};
+hipError_t dev_alloc(void** p, size_t bytes) {
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e == hipSuccess) {
+    g_allocs.fetch_add(1, std::memory_order_relaxed);
+    g_alloc_bytes.fetch_add(bytes, std::memory_order_relaxed);
+  }
+  return e;
+}
+hipError_t dev_alloc_async(void** p, size_t bytes, hipStream_t st) {
+  const hipError_t e = hipMallocAsync(p, bytes, st);
+  if (e == hipSuccess) {
+    g_allocs.fetch_add(1, std::memory_order_relaxed);
+    g_alloc_bytes.fetch_add(bytes, std::memory_order_relaxed);
+  }
+  return e;
+}
+hipError_t host_alloc(void** p, size_t bytes) {
+  const hipError_t e = hipHostMalloc(p, bytes, hipHostMallocDefault);
+  if (e == hipSuccess) {
+    g_allocs.fetch_add(1, std::memory_order_relaxed);
+    g_alloc_bytes.fetch_add(bytes, std::memory_order_relaxed);
+  }
+  return e;
+}
+
 }  // namespace rtg
+
+// Grow-only device scratch of a scene's renders (stack spill, wave trace, tile ring or chunk partial sums).
+// Renders of one scene never overlap — rtg_render refuses while one is pending, collect_stats waits for
+// its stream, a failed render waits for it (SyncOnError) — so a buffer is idle whenever a render starts,
+// and frames allocate nothing once the buffers reached their sizes (config 2: 0.8 GB of partials, config
+// 5: 6.3 GB, kept with the scene; 288 GB of HBM).
+struct ScratchBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
 
 struct rtg_scene {
   int device = 0;
@@ -866,6 +901,7 @@ struct rtg_scene {
   size_t host_stage_bytes = 0;
   float* dev_out = nullptr;  // device frame of host-output renders (kept between renders)
   size_t dev_out_bytes = 0;
+  ScratchBuf scr_spill, scr_trace, scr_partial;  // render scratch (ScratchBuf)
   float* pending_host_out = nullptr;
   size_t pending_host_bytes = 0;
   // hot treelet (schedule 5): the node array is renumbered so the nodes a probe render of this
@@ -944,6 +980,12 @@ rtg_status rtg_bvh_build_host(const rtg_scene_desc* desc, rtg_bvh_node_host* nod
   return RTG_OK;
 }
 
+rtg_status rtg_allocation_count(uint64_t* count, uint64_t* bytes) {
+  if (count) *count = g_allocs.load(std::memory_order_relaxed);
+  if (bytes) *bytes = g_alloc_bytes.load(std::memory_order_relaxed);
+  return RTG_OK;
+}
+
 rtg_status rtg_bvh_node_order(const double* boxes, int64_t n, int64_t* order) {
   if (n < 0 || (n > 0 && (!boxes || !order))) return fail(RTG_E_INVALID, "null array or negative count");
   try {
@@ -1018,16 +1060,16 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc_in, int32_t device, rtg_s
     rtg_scene_destroy(s);
     return st;
   };
-  hipError_t e = hipMalloc(&s->dmem, total);
+  hipError_t e = dev_alloc(&s->dmem, total);
   if (e != hipSuccess) return cleanup(hip_fail(e, "hipMalloc(scene)"));
   s->dbytes = total;
   if ((e = hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking)) != hipSuccess)
     return cleanup(hip_fail(e, "hipStreamCreate"));
   if ((e = hipEventCreate(&s->ev0)) != hipSuccess || (e = hipEventCreate(&s->ev1)) != hipSuccess)
     return cleanup(hip_fail(e, "hipEventCreate"));
-  if ((e = hipMalloc(&s->counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
+  if ((e = dev_alloc(reinterpret_cast<void**>(&s->counters), kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return cleanup(hip_fail(e, "hipMalloc(counters)"));
-  if ((e = hipHostMalloc(&s->host_counters, kNumCounters * sizeof(unsigned long long))) != hipSuccess)
+  if ((e = host_alloc(reinterpret_cast<void**>(&s->host_counters), kNumCounters * sizeof(unsigned long long))) != hipSuccess)
     return cleanup(hip_fail(e, "hipHostMalloc(counters)"));
   char* base = static_cast<char*>(s->dmem);
   {
@@ -1046,7 +1088,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc_in, int32_t device, rtg_s
     size_t end = 0;
     for (const Src& x : srcs) end = std::max(end, x.off + x.bytes);
     void* stage = nullptr;
-    if (end > 0 && hipHostMalloc(&stage, end, hipHostMallocDefault) == hipSuccess) {
+    if (end > 0 && host_alloc(&stage, end) == hipSuccess) {
       char* st = static_cast<char*>(stage);
       host_par_for(static_cast<int64_t>(srcs.size()), [&](int64_t b, int64_t e2, int) {
         for (int64_t k = b; k < e2; ++k) std::memcpy(st + srcs[k].off, srcs[k].p, srcs[k].bytes);
@@ -1069,7 +1111,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc_in, int32_t device, rtg_s
   if (hs.gpu_bvh && nrefs > 0) {  // RTG_BVH_GPU: build the nodes and leaf-ordered refs here
     int32_t* refs_dev = reinterpret_cast<int32_t*>(base + parts[1].off);
     int32_t* sorted = nullptr;
-    if ((e = hipMallocAsync(reinterpret_cast<void**>(&sorted), nrefs * 4, s->own_stream)) != hipSuccess)
+    if ((e = dev_alloc_async(reinterpret_cast<void**>(&sorted), nrefs * 4, s->own_stream)) != hipSuccess)
       return cleanup(hip_fail(e, "hipMalloc(bvh refs)"));
     GpuBvhResult r{};
     e = gpu_build_bvh4(reinterpret_cast<const float4*>(base + parts[2].off),
@@ -1177,6 +1219,8 @@ void rtg_scene_destroy(rtg_scene* s) {
   if (s->host_counters) (void)hipHostFree(s->host_counters);
   if (s->host_stage) (void)hipHostFree(s->host_stage);
   if (s->dev_out) (void)hipFree(s->dev_out);
+  for (ScratchBuf* b : {&s->scr_spill, &s->scr_trace, &s->scr_partial})
+    if (b->p) (void)hipFree(b->p);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
   if (s->ev1) (void)hipEventDestroy(s->ev1);
   if (s->own_stream) (void)hipStreamDestroy(s->own_stream);
@@ -1338,7 +1382,15 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   // costs the render loop time (config 5 +2.0 %, config 2 +7.5 %, config 4 +17 %: DESIGN.md §9), the
   // full-frame buffers cost memory. RTG_TILE_SLOTS=0 / >0 forces it off / on.
   const int64_t full_partial_bytes = int64_t(rows) * W * 12 * dj.chunks;
-  const bool ring_on = K.tile_slots > 0 || (K.tile_slots < 0 && full_partial_bytes > kRingAutoBytes);
+  // ... and at most half of the device memory free to this scene (the partials it already holds count as
+  // free: they are reused), so a smaller or busier device takes the ring instead of failing
+  int64_t ring_auto = kRingAutoBytes;
+  if (K.tile_slots < 0 && full_partial_bytes > (int64_t(1) << 30)) {
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(s->device) == hipSuccess && hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+      ring_auto = std::min<int64_t>(ring_auto, static_cast<int64_t>((free_b + s->scr_partial.bytes) / 2));
+  }
+  const bool ring_on = K.tile_slots > 0 || (K.tile_slots < 0 && full_partial_bytes > ring_auto);
   // the ring kernels index the frame with 32-bit byte offsets (ring_combine's buffer descriptor: the
   // shard's frame below 2 GiB) and pack a tile into 25 bits of the per-wave batch table (tile << 7):
   // larger shards keep the full-frame partials, whose indexing is 64-bit
@@ -1550,8 +1602,8 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   const int64_t rows = (cp.image_height - 1 - j2.row_begin) / j2.row_stride + 1;
   uint32_t* visits = nullptr;
   float* out = nullptr;
-  RTG_HIP(hipMalloc(reinterpret_cast<void**>(&visits), n * 4), "hipMalloc(node visits)");
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(&out), rows * cp.image_width * 12);
+  RTG_HIP(dev_alloc(reinterpret_cast<void**>(&visits), n * 4), "hipMalloc(node visits)");
+  hipError_t e = dev_alloc(reinterpret_cast<void**>(&out), rows * cp.image_width * 12);
   // the probe runs on the scene's own (non-blocking) stream: every copy here is ordered on it
   hipStream_t os = s->own_stream;
   if (e == hipSuccess) e = hipMemsetAsync(visits, 0, n * 4, os);
@@ -1585,7 +1637,7 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
     return fail(RTG_E_INVALID, "hot treelet: a BVH inner code outside the node array (corrupt tree)");
   }
   void* stage = nullptr;  // the renumbered array through pinned memory (one DMA), else from the vector
-  if (hipHostMalloc(&stage, n * nb, hipHostMallocDefault) == hipSuccess) {
+  if (host_alloc(&stage, n * nb) == hipSuccess) {
     std::memcpy(stage, rec.data(), n * nb);
     e = hipMemcpyAsync(const_cast<float4*>(s->dev.nodes), stage, n * nb, hipMemcpyHostToDevice, os);
   } else {
@@ -1758,20 +1810,29 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
       if (s->dev_out) RTG_HIP(hipFree(s->dev_out), "hipFree(out)");
       s->dev_out = nullptr;
       s->dev_out_bytes = 0;
-      RTG_HIP(hipMalloc(reinterpret_cast<void**>(&s->dev_out), out_bytes), "hipMalloc(out)");
+      RTG_HIP(dev_alloc(reinterpret_cast<void**>(&s->dev_out), out_bytes), "hipMalloc(out)");
       s->dev_out_bytes = out_bytes;
     }
     dout = s->dev_out;
   }
   dj.out = dout;
-  StreamScratch scratch;
-  scratch.stream = stream;
+  SyncOnError sync_on_error;
+  sync_on_error.stream = stream;
+  auto grow = [](ScratchBuf& b, size_t need, const char* what) -> rtg_status {
+    if (b.p && b.bytes >= need) return RTG_OK;
+    if (b.p) RTG_HIP(hipFree(b.p), "hipFree(scratch)");  // device-synchronous: nothing still reads it
+    b.p = nullptr;
+    b.bytes = 0;
+    RTG_HIP(dev_alloc(&b.p, std::max<size_t>(need, 256)), what);
+    b.bytes = need;
+    return RTG_OK;
+  };
   dj.spill = nullptr;
   if (dj.spill_depth > 0) {
-    RTG_HIP(hipMallocAsync(scratch.add(),
-                           static_cast<size_t>(P.grid_waves) * 64 * dj.spill_depth * sizeof(int32_t), stream),
-            "hipMallocAsync(stack spill)");
-    dj.spill = static_cast<int32_t*>(scratch.ptr[scratch.n - 1]);
+    pst = grow(s->scr_spill, static_cast<size_t>(P.grid_waves) * 64 * dj.spill_depth * sizeof(int32_t),
+               "hipMalloc(stack spill)");
+    if (pst != RTG_OK) return pst;
+    dj.spill = static_cast<int32_t*>(s->scr_spill.p);
   }
   dj.counters = s->counters;
   RTG_HIP(hipMemsetAsync(s->counters, 0, kNumCounters * sizeof(unsigned long long), stream), "hipMemsetAsync");
@@ -1780,20 +1841,20 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   int64_t trace_slots = 0;
   if (trace) {
     trace_slots = int64_t(P.grid_waves);
-    RTG_HIP(hipMallocAsync(scratch.add(), trace_slots * 32, stream), "hipMalloc(trace)");
-    dj.trace = static_cast<unsigned long long*>(scratch.ptr[scratch.n - 1]);
+    if ((pst = grow(s->scr_trace, trace_slots * 32, "hipMalloc(trace)")) != RTG_OK) return pst;
+    dj.trace = static_cast<unsigned long long*>(s->scr_trace.p);
     RTG_HIP(hipMemsetAsync(dj.trace, 0, trace_slots * 32, stream), "hipMemset(trace)");
   }
   if (P.chunked && P.ring_slots) {  // [slot words: gen R, ticket R][ring of tile slots]
-    RTG_HIP(hipMallocAsync(scratch.add(), P.ring_bytes, stream), "hipMallocAsync(tile ring)");
-    unsigned char* base = static_cast<unsigned char*>(scratch.ptr[scratch.n - 1]);
+    if ((pst = grow(s->scr_partial, P.ring_bytes, "hipMalloc(tile ring)")) != RTG_OK) return pst;
+    unsigned char* base = static_cast<unsigned char*>(s->scr_partial.p);
     const size_t words = size_t(8) * P.ring_slots;  // a multiple of 16 B at the allocation's start
     RTG_HIP(hipMemsetAsync(base, 0, words, stream), "hipMemsetAsync(tile ring words)");
     dj.ring_words = reinterpret_cast<uint32_t*>(base);
     dj.partial = reinterpret_cast<float*>(base + words);
   } else if (P.chunked) {
-    RTG_HIP(hipMallocAsync(scratch.add(), out_bytes * dj.chunks, stream), "hipMallocAsync(partial sums)");
-    dj.partial = static_cast<float*>(scratch.ptr[scratch.n - 1]);
+    if ((pst = grow(s->scr_partial, out_bytes * dj.chunks, "hipMalloc(partial sums)")) != RTG_OK) return pst;
+    dj.partial = static_cast<float*>(s->scr_partial.p);
   }
   if (P.skip_kernel)
     RTG_HIP(hipMemsetAsync(dj.partial + static_cast<size_t>(dj.chunk_begin) * rows * W * 3, 0,
@@ -1853,13 +1914,14 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
       if (s->host_stage) RTG_HIP(hipHostFree(s->host_stage), "hipHostFree(stage)");
       s->host_stage = nullptr;
       s->host_stage_bytes = 0;
-      RTG_HIP(hipHostMalloc(&s->host_stage, out_bytes), "hipHostMalloc(stage)");
+      RTG_HIP(host_alloc(&s->host_stage, out_bytes), "hipHostMalloc(stage)");
       s->host_stage_bytes = out_bytes;
     }
     RTG_HIP(hipMemcpyAsync(s->host_stage, dout, out_bytes, hipMemcpyDeviceToHost, stream), "hipMemcpy(out)");
     s->pending_host_out = out_rgb;
     s->pending_host_bytes = out_bytes;
   }
+  sync_on_error.committed = true;
   s->pending = true;
   s->pending_stream = stream;
   {

@@ -80,13 +80,20 @@ struct rtg_comm {
   std::vector<int32_t> ranks, devices;  // per local rank
   std::vector<ncclComm_t> comms;
   std::vector<hipStream_t> streams;     // the communicator's own stream per local rank
-  // scratch, grown on demand: per-rank shard buffers and the root frame of rtg_render_frame (the
-  // gather's staging buffer is allocated per call, stream-ordered, so concurrent gathers never share it)
+  // scratch, grown on demand and kept: per-rank shard buffers and the root frame of rtg_render_frame, and
+  // the root's gather staging buffer (rtg_gather_rows), so steady-state frames allocate nothing (VERDICT
+  // r05 item 4). `stage_done` is recorded behind each gather's de-interleave: a gather on another stream
+  // first waits for it, so gathers in flight on two streams take turns at the buffer instead of sharing it.
   std::vector<void*> shard;
   std::vector<size_t> shard_bytes;
   void* frame = nullptr;
   size_t frame_bytes = 0;
   int32_t frame_local = -1;  // local rank whose device holds `frame`
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+  int32_t stage_local = -1;       // local rank whose device holds `stage`
+  hipEvent_t stage_done = nullptr;  // on stage_local's device; recorded once a gather used the buffer
+  bool stage_used = false;
 
   int32_t local_of(int32_t rank) const {
     for (size_t i = 0; i < ranks.size(); ++i)
@@ -120,7 +127,7 @@ rtg_status ensure(void** p, size_t* have, size_t bytes, int32_t device, const ch
   if (*p) COMM_HIP(hipFree(*p), "hipFree(comm scratch)");
   *p = nullptr;
   *have = 0;
-  COMM_HIP(hipMalloc(p, std::max<size_t>(bytes, 16)), what);
+  COMM_HIP(dev_alloc(p, std::max<size_t>(bytes, 16)), what);
   *have = bytes;
   return RTG_OK;
 }
@@ -214,6 +221,11 @@ void rtg_comm_destroy(rtg_comm* c) {
     (void)hipSetDevice(c->devices[c->frame_local]);
     (void)hipFree(c->frame);
   }
+  if (c->stage_local >= 0) {
+    (void)hipSetDevice(c->devices[c->stage_local]);
+    if (c->stage) (void)hipFree(c->stage);  // hipFree waits for the device: no gather still reads it
+    if (c->stage_done) (void)hipEventDestroy(c->stage_done);
+  }
   for (ncclComm_t m : c->comms)
     if (m) (void)ncclCommDestroy(m);
   for (size_t i = 0; i < c->streams.size(); ++i)
@@ -271,49 +283,59 @@ rtg_status rtg_gather_rows(rtg_comm* c, const void* const* shards, int32_t heigh
   auto stream_of = [&](int32_t i) {
     return (streams && streams[i]) ? static_cast<hipStream_t>(streams[i]) : c->streams[i];
   };
-  // the root's staging buffer: allocated on the root's stream for this call and freed behind the
-  // de-interleave on the same stream (stream-ordered), so two gathers in flight on different streams
-  // (double-buffered frames) each have their own
+  // the root's staging buffer, grown on demand and kept (rtg_comm::stage); the root's stream waits for the
+  // previous gather's de-interleave (whatever stream that ran on) before RCCL writes into it
   void* stage = nullptr;
   if (rl >= 0) {
     COMM_HIP(hipSetDevice(c->devices[rl]), "hipSetDevice");
-    COMM_HIP(hipMallocAsync(&stage, std::max<size_t>(block * N, 16), stream_of(rl)), "hipMallocAsync(gather stage)");
-  }
-  auto release_stage = [&]() {
-    if (stage) {
-      (void)hipSetDevice(c->devices[rl]);
-      (void)hipFreeAsync(stage, stream_of(rl));  // error path: the enqueue error is what gets reported
+    const size_t need = std::max<size_t>(block * N, 16);
+    if (c->stage_local != rl || c->stage_bytes < need || !c->stage) {
+      if (c->stage_local >= 0) {  // regrow (or a new root): free the old buffer once nothing reads it
+        COMM_HIP(hipSetDevice(c->devices[c->stage_local]), "hipSetDevice");
+        if (c->stage_used) COMM_HIP(hipEventSynchronize(c->stage_done), "hipEventSynchronize(gather stage)");
+        if (c->stage) COMM_HIP(hipFree(c->stage), "hipFree(gather stage)");
+        if (c->stage_done) COMM_HIP(hipEventDestroy(c->stage_done), "hipEventDestroy");
+        c->stage = nullptr;
+        c->stage_done = nullptr;
+        c->stage_bytes = 0;
+        c->stage_used = false;
+        c->stage_local = -1;
+        COMM_HIP(hipSetDevice(c->devices[rl]), "hipSetDevice");
+      }
+      COMM_HIP(hipEventCreateWithFlags(&c->stage_done, hipEventDisableTiming), "hipEventCreate");
+      c->stage_local = rl;
+      COMM_HIP(dev_alloc(&c->stage, need), "hipMalloc(gather stage)");
+      c->stage_bytes = need;
+    } else if (c->stage_used) {
+      COMM_HIP(hipStreamWaitEvent(stream_of(rl), c->stage_done, 0), "hipStreamWaitEvent(gather stage)");
     }
-  };
+    stage = c->stage;
+  }
   if (const ncclResult_t r = ncclGroupStart(); r != ncclSuccess) {
-    release_stage();
     return nccl_err(r, "ncclGroupStart");
   }
   for (int32_t i = 0; i < nlocal; ++i) {
     const hipError_t e = hipSetDevice(c->devices[i]);
     if (e != hipSuccess) {
       (void)ncclGroupEnd();
-      release_stage();
-      return hip_err(e, "hipSetDevice");
+        return hip_err(e, "hipSetDevice");
     }
     const ncclResult_t r = ncclGather(shards[i], i == rl ? stage : nullptr, block, ncclUint8, root, c->comms[i],
                                       stream_of(i));
     if (r != ncclSuccess) {
       (void)ncclGroupEnd();
-      release_stage();
-      return nccl_err(r, "ncclGather");
+        return nccl_err(r, "ncclGather");
     }
   }
   if (const ncclResult_t r = ncclGroupEnd(); r != ncclSuccess) {
-    release_stage();
     return nccl_err(r, "ncclGroupEnd");
   }
   if (rl >= 0) {
     COMM_HIP(hipSetDevice(c->devices[rl]), "hipSetDevice");
     const hipError_t e = launch_deinterleave(stage, out, N, height, row_bytes, stream_of(rl));
-    const hipError_t ef = hipFreeAsync(stage, stream_of(rl));
     if (e != hipSuccess) return hip_err(e, "de-interleave kernel launch");
-    if (ef != hipSuccess) return hip_err(ef, "hipFreeAsync(gather stage)");
+    COMM_HIP(hipEventRecord(c->stage_done, stream_of(rl)), "hipEventRecord(gather stage)");
+    c->stage_used = true;
   }
   return RTG_OK;
 }

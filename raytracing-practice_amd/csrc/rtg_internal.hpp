@@ -127,6 +127,10 @@ bool build_bvh(const rtg_scene_desc* desc, Bvh* out, std::string* err);
 void bvh_node_order(const double* boxes6, int64_t n, int64_t* order);
 bool compile_scene(const rtg_scene_desc* desc, HostScene* out, std::string* err);
 void resolve_camera(const rtg_camera_desc* cam, rtg_camera_params* out);
+// Counted allocations (rtg_allocation_count; rtg_api.cpp): every device / pinned-host buffer of the library
+hipError_t dev_alloc(void** p, size_t bytes);
+hipError_t dev_alloc_async(void** p, size_t bytes, hipStream_t st);
+hipError_t host_alloc(void** p, size_t bytes);
 // rtg_last_error() text of the calling thread; returns `code` (rtg_api.cpp)
 rtg_status set_last_error(rtg_status code, const std::string& msg);
 

@@ -144,7 +144,8 @@ RTG_SYMBOLS = ("rtg_abi_version", "rtg_last_error", "rtg_device_count", "rtg_cam
                "rtg_comm_unique_id", "rtg_comm_create_rank", "rtg_comm_size", "rtg_comm_destroy",
                "rtg_gather_rows", "rtg_deinterleave_rows", "rtg_render_frame", "rtg_render_plan",
                "rtg_shard_layout", "rtg_deinterleave_rows_host", "rtg_scene_prepare",
-               "rtg_hot_treelet_order_host", "rtg_bvh_node_order")
+               "rtg_hot_treelet_order_host", "rtg_bvh_node_order",
+               "rtg_allocation_count")
 RTG_COMM_ID_BYTES = 128
 
 
@@ -228,12 +229,13 @@ class Library:
         L.rtg_shard_layout.argtypes = [C.c_int32, C.c_int32, C.c_int32] + [_P(C.c_int32)] * 4
         L.rtg_deinterleave_rows_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int64]
         L.rtg_bvh_node_order.argtypes = [C.c_void_p, C.c_int64, C.c_void_p]
+        L.rtg_allocation_count.argtypes = [_P(C.c_uint64), _P(C.c_uint64)]
         for name in ("rtg_device_count", "rtg_camera_resolve", "rtg_scene_create",
                      "rtg_scene_get_info", "rtg_render", "rtg_render_wait", "rtg_resolve_rgb8",
                      "rtg_bvh_build_host", "rtg_comm_create_local", "rtg_comm_unique_id",
                      "rtg_comm_create_rank", "rtg_comm_size", "rtg_gather_rows", "rtg_deinterleave_rows",
                      "rtg_render_frame", "rtg_render_plan", "rtg_shard_layout", "rtg_deinterleave_rows_host",
-                     "rtg_bvh_node_order"):
+                     "rtg_bvh_node_order", "rtg_allocation_count"):
             getattr(L, name).restype = C.c_int32
         if L.rtg_abi_version() != RTG_ABI_VERSION:
             raise RuntimeError("librtgpu ABI version mismatch")
@@ -272,6 +274,12 @@ class Library:
         out = np.empty(len(b), dtype=np.int64)
         self.check("rtg_bvh_node_order", self.lib.rtg_bvh_node_order(b.ctypes.data, len(b), out.ctypes.data))
         return out
+
+    def allocation_count(self):
+        """rtg_allocation_count: (allocations, bytes) the library made in this process so far."""
+        n, b = C.c_uint64(0), C.c_uint64(0)
+        self.check("rtg_allocation_count", self.lib.rtg_allocation_count(C.byref(n), C.byref(b)))
+        return n.value, b.value
 
     def scene_create(self, desc: rtg_scene_desc, device: int = 0) -> "DeviceScene":
         h = C.c_void_p()

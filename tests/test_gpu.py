@@ -1022,9 +1022,53 @@ def test_comm_world_of_one(gpu_lib, scenes):
     ds.close()
 
 
+def test_frames_allocate_nothing_after_the_first(gpu_lib, scenes):
+    """the C-ABI frame path keeps its buffers (the scene's render scratch and output,
+    the communicator's shard, frame and gather staging buffers), so after the first frame neither
+    rtg_render_frame nor rtg_gather_rows nor a chunked rtg_render allocates anything
+    (rtg_allocation_count counts every device / pinned allocation of the library). World of one."""
+    import torch
+
+    s = scenes.build("bouncing_spheres", rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 96, 40, 20  # 3 chunks: partial sums in use
+    ds = gpu_lib.scene_create(s.desc)
+    comm = gpu_lib.comm_local([0])
+    frames, counts = [], []
+    for k in range(5):
+        f, _ = comm.render_frame([ds], c, seed=3)
+        frames.append(f)
+        counts.append(gpu_lib.allocation_count()[0])
+    assert counts[1:] == [counts[0]] * 4, counts
+    assert all(np.array_equal(f, frames[0]) for f in frames)
+    ref, _ = ds.render_host(c, seed=3)
+    assert np.array_equal(ref, frames[0])
+    comm2 = gpu_lib.comm_rank(gpu_lib.comm_unique_id(), 1, 0, 0)
+    H, W = ref.shape[:2]
+    shard = torch.from_numpy(ref).cuda()
+    out = torch.zeros_like(shard)
+    stream = torch.cuda.current_stream().cuda_stream
+    torch.cuda.synchronize()
+    counts = []
+    for k in range(5):
+        comm2.gather_rows([shard.data_ptr()], H, W * 12, 0, out.data_ptr(), [stream])
+        counts.append(gpu_lib.allocation_count()[0])
+    torch.cuda.synchronize()
+    assert counts[1:] == [counts[0]] * 4, counts
+    assert np.array_equal(out.cpu().numpy(), ref)
+    n0 = gpu_lib.allocation_count()[0]
+    for k in range(3):
+        g, _ = ds.render_host(c, seed=3)
+    assert gpu_lib.allocation_count()[0] == n0 and np.array_equal(g, ref)
+    comm2.close()
+    comm.close()
+    ds.close()
+
+
 def test_gathers_in_flight_on_two_streams(gpu_lib, scenes):
-    """rtg_gather_rows stages each call in its own stream-ordered buffer: two gathers of
-    different frames enqueued back to back on two streams both land intact."""
+    """rtg_gather_rows's staging buffer belongs to the communicator (ABI 7: kept between gathers); a
+    gather on another stream waits for the previous one's de-interleave first: two gathers of different
+    frames enqueued back to back on two streams both land intact."""
     import torch
 
     s = scenes.build("bouncing_spheres", rand_seed=1)

@@ -1682,6 +1682,9 @@ rtg_status ensure_origin_bound(rtg_scene* s, const rtg_camera_desc* cam, hipStre
   RTG_HIP(launch_repad(reinterpret_cast<float*>(const_cast<float4*>(s->dev.nodes)), s->dev.num_nodes,
                        s->dev.node_width, delta, stream),
           "repad kernel launch");
+  // synchronous: work on another stream (rtg_scene_prepare's probe and node download with a
+  // NULL stream, a later render elsewhere) must see the repadded boxes; a camera moving outward is rare
+  RTG_HIP(hipStreamSynchronize(stream), "repad kernel");
   s->origin_bound = target;
   s->host_nodes.clear();  // the hot treelet downloads the repadded array when it next tunes
   if (s->knobs.verbose) std::fprintf(stderr, "[rtg] culling margin widened for origins up to %.6g\n", target);

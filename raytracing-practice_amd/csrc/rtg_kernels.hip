@@ -294,6 +294,18 @@ __device__ __forceinline__ const int32_t* tie_ranks_late() {
   const volatile DevScene* ks = (const volatile DevScene*)(__builtin_amdgcn_kernarg_segment_ptr());
   return ks->tie_rank;
 }
+// The counting (COUNT) kernels check that assumption at every tie: a kernel whose first argument
+// is not its DevScene reads another pointer there, reported as a corrupt render (rtg_render: RTG_E_INVALID);
+// they then use S.tie_rank itself
+template <bool COUNT>
+__device__ __forceinline__ const int32_t* tie_ranks_at_tie(const DevScene& S, bool& corrupt) {
+  const int32_t* r = tie_ranks_late();
+  if (COUNT && r != S.tie_rank) {
+    corrupt = true;
+    return S.tie_rank;
+  }
+  return r;
+}
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
@@ -671,8 +683,10 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       // exact-t tie (rare; a wave-uniform branch): the sphere earlier in the list wins, as the reference's list
       // walk keeps the first sphere at a t (interval::surrounds); the ranks are read only then (tie_ranks_late)
       bool take = th > 0.0f && th < t.tbest;
-      if (ballot_tie(th == t.tbest) != 0 && th == t.tbest)
-        take = tie_ranks_late()[first + k] < tie_ranks_late()[t.best];
+      if (ballot_tie(th == t.tbest) != 0 && th == t.tbest) {
+        const int32_t* rk = tie_ranks_at_tie<COUNT>(S, corrupt);
+        take = rk[first + k] < rk[t.best];
+      }
       if (take) {
         t.tbest = th;
         t.best = first + k;
@@ -709,8 +723,10 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
       if (MAT) m = ibits(sp4[1].w);
       take = th > 0.0f && th < t.tbest;
       // exact-t tie: a sphere replaces only an equal-t sphere later in the list (never a quad)
-      if (ballot_tie(th == t.tbest) != 0 && th == t.tbest)
-        take = !(t.best & kQuadRefBit) && tie_ranks_late()[ref] < tie_ranks_late()[t.best];
+      if (ballot_tie(th == t.tbest) != 0 && th == t.tbest) {
+        const int32_t* rk = tie_ranks_at_tie<COUNT>(S, corrupt);
+        take = !(t.best & kQuadRefBit) && rk[ref] < rk[t.best];
+      }
     }
     if (take) {  // th > tmin >= 0.001 on a hit
       t.tbest = th;

@@ -671,6 +671,11 @@ class FrameGather:
             dist.gather(shard, dst=self.dst)
             return None
         dist.gather(shard, gather_list=self.parts, dst=self.dst)
+        return self.deinterleave(stream_ptr)
+
+    def deinterleave(self, stream_ptr: Optional[int] = None):
+        """The staging blocks -> the frame: the library's kernel for device tensors (on stream_ptr), its
+        host twin for CPU tensors (test_gpu checks the two agree)."""
         if self.stage.is_cuda:
             self.lib.deinterleave_rows(self.device, self.stage.data_ptr(), self.frame.data_ptr(), self.world,
                                        self.height, self.row_bytes, stream_ptr)

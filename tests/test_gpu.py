@@ -668,6 +668,11 @@ def test_bvh_node_world_ties_follow_leaf_order(gpu_lib, scenes, oracle, bvh):
         o, segs = oracle.render_f32(s.desc, cam)
         assert np.array_equal(g, o) and st.segments == segs, (key, float(np.mean(np.all(g == o, axis=-1))))
         frames[key] = g
+        if bvh == rtgpu.RTG_BVH_SAH:  # the counting kernel checks where it reads the ranks at a tie
+            ds = gpu_lib.scene_create(s.desc)
+            gc, _ = ds.render_host(cam, count=True)
+            ds.close()
+            assert np.array_equal(gc, g)
     differ = int(np.sum(np.any(frames["bvh_node"] != frames["list"], axis=-1)))
     assert differ > 200, differ  # 255 of the 96 x 64 pixels on the MI355X (tie regions)
 
@@ -1020,6 +1025,56 @@ def test_comm_world_of_one(gpu_lib, scenes):
     comm2.close()
     comm.close()
     ds.close()
+
+
+def test_far_camera_repad_then_prepare_on_another_stream(gpu_lib, scenes, oracle):
+    """a camera beyond twice the primitives' reach makes a render widen the culling margin on the
+    device (the repad) on the render's stream; rtg_scene_prepare with a NULL stream then downloads the node
+    array for the hot treelet and uploads it renumbered. The repad is synchronous, so that download already
+    holds the widened boxes and the plan's origin_bound is true of the device array: renders of the far
+    camera after the prepare are cpu_ref32's frames bit for bit (treelet schedule, 14k spheres)."""
+    import torch
+
+    s = scenes.build("bouncing_spheres", grid=60)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(s.camera)
+    c.image_width, c.aspect_ratio, c.samples_per_pixel, c.max_depth = 64, 16.0 / 9.0, 2, 8
+    c.lookfrom, c.lookat, c.vfov, c.defocus_angle = rtgpu.D3(4500.0, 800.0, 900.0), rtgpu.D3(0.0, 0.0, 0.0), 1.0, 0.0
+    ds = gpu_lib.scene_create(s.desc)
+    assert ds.plan(c).schedule == 5
+    bound0 = ds.plan(c).origin_bound
+    out = torch.zeros((36, 64, 3), dtype=torch.float32, device="cuda")
+    user = torch.cuda.Stream()
+    ds.render_device(c, out.data_ptr(), user.cuda_stream)
+    assert ds.plan(c).origin_bound > bound0 >= 0
+    c2 = rtgpu.rtg_camera_desc.from_buffer_copy(c)
+    c2.lookat = rtgpu.D3(10.0, 0.0, 5.0)  # another camera: the prepare re-tunes (downloads the nodes)
+    ds.prepare(c2)
+    g, st = ds.render_host(c)
+    o, segs = oracle.render_f32(s.desc, c)
+    torch.cuda.synchronize()
+    assert np.array_equal(g, o) and st.segments == segs
+    assert np.array_equal(out.cpu().numpy(), o)
+    ds.close()
+
+
+@pytest.mark.parametrize("world,height", [(2, 5), (3, 7), (8, 21)])
+def test_frame_gather_device_deinterleave(gpu_lib, world, height):
+    """bench.py's timed N > 1 gather (rtgpu.FrameGather) de-interleaves CUDA staging blocks with
+    the library's kernel on the stream; the CPU tests only reach the host twin. Here the staging blocks are
+    filled by hand (every element its own value, the padding rows included) and FrameGather's CUDA step must
+    give the host twin's frame exactly."""
+    import torch
+
+    padded, W = -(-height // world), 5
+    fg = rtgpu.FrameGather.__new__(rtgpu.FrameGather)  # no process group: the dst rank's state set up by hand
+    fg.lib, fg.height, fg.dst, fg.device, fg.world, fg.rank = gpu_lib, height, 0, 0, world, 0
+    fg.shape, fg.row_bytes = (padded, W, 3), W * 3 * 4
+    fg.stage = torch.arange(world * padded * W * 3, dtype=torch.float32, device="cuda").reshape(world, padded, W, 3)
+    fg.frame = torch.full((height, W, 3), -1.0, device="cuda")
+    out = fg.deinterleave(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    want = gpu_lib.deinterleave_rows_host(fg.stage.cpu().numpy().reshape(world * padded, W, 3), world, height)
+    assert want.shape == (height, W, 3) and np.array_equal(out.cpu().numpy(), want)
 
 
 def test_frames_allocate_nothing_after_the_first(gpu_lib, scenes):

@@ -1523,13 +1523,15 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   if (P->skip_kernel || variant != 3) lds4 = -1;
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
-                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks, j4.lds_ring};
+                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks, j4.lds_ring,
+                          j4.lds_pairs};
     j4 = dj;
     j4.lds_waves = 4;
     j4.lds_nodes = l4[0], j4.lds_refs = l4[1], j4.lds_spheres = l4[2], j4.lds_quads = l4[3];
     j4.lds_materials = l4[4], j4.lds_textures = l4[5], j4.lds_perlin_vec = l4[6], j4.lds_perlin_perm = l4[7];
     j4.lds_stacks = l4[8];
     j4.lds_ring = l4[9];
+    j4.lds_pairs = l4[10];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
   P->j4 = j4;

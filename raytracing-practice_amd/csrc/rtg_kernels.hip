@@ -32,6 +32,11 @@
 namespace rtg {
 namespace {
 
+// leaf trips of sphere-only scenes spread their (ray, sphere) pairs over the wave (leaf_pairs); 0 builds the
+// one-sphere-per-lane trip (A/B)
+#ifndef RTG_LEAF_PAIRS
+#define RTG_LEAF_PAIRS 1
+#endif
 constexpr float kTMin = 0.001f;  // interval(0.001, infinity), camera.hpp:192
 // Conservative culling. Box tests only prune: a child is skipped when
 // its entry distance is past fmaf(tbest, kCullRel, kCullAbs) or its exit before kCullTMin, a margin at
@@ -1039,6 +1044,103 @@ __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w
   if (__any(w.corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
 }
 
+// Leaf trip with the leaf lanes' (ray, sphere) pairs spread over the whole wave (VERDICT r05 items 2-3;
+// sphere-only scenes, whose leaf refs are the identity). In a leaf trip only the lanes waiting at a leaf
+// (about a third of the wave on book-1 and the 1M field) test a sphere, one per trip, and a leaf of n
+// spheres costs its lane n trips. Here every pending pair of the trip gets a lane of its own: the leaf
+// lanes' counts are prefix-summed (bit planes of n through ballot + mbcnt), each owner writes its lane id
+// into the wave's 64-byte owner table (LDS) at its pair slots [pre, pre + n), every lane below the total
+// reads its owner there and fetches the owner's ray with ds_bpermute, tests its sphere (unbounded above),
+// and each owner reads its pairs' roots back in leaf order and applies them as the one-at-a-time walk
+// would (a root past the owner's current tbest is a miss there too, and the exact-t tie rule compares the
+// same roots in the same order), so frames are those of leaf_step. Pairs past the
+// 64th stay with their owner (its leaf code advanced) for the next leaf trip. Called by the whole wave.
+typedef __attribute__((address_space(3))) uint8_t lu8;
+__device__ __forceinline__ float bperm_f(int src, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ int bperm_i(int src, int v) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+template <class Stk, bool COUNT, bool CHECK, bool MAT>
+__device__ __forceinline__ void leaf_pairs(Trav& t, const DevScene& S, V3 o, V3 d, float time, const Stk& stk,
+                                           Counts<COUNT>& cnt, bool& corrupt, lu8* otab) {
+  const int lane = __lane_id();
+  int32_t first = 0, n = 0;
+  if (t.todo < 0) {
+    const int32_t code = ~t.todo;
+    first = code >> 3;
+    n = (code & 7) + 1;
+    if ((CHECK || COUNT) && static_cast<int64_t>(first) + n > S.num_refs) {
+      corrupt = true;
+      t.todo = kTravDone;
+      n = 0;
+    }
+  }
+  // exclusive prefix of n over the lanes, and the trip's pair total, from n's four bit planes (n <= 8)
+  uint32_t pre = 0, total = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint64_t m = ballot(((n >> b) & 1) != 0);
+    pre += lanes_below(m) << b;
+    total += static_cast<uint32_t>(__popcll(m)) << b;
+  }
+  for (int j = 0; j < 8; ++j) {
+    if (ballot(j < n && pre + j < 64u) == 0) break;
+    if (j < n && pre + j < 64u) otab[pre + j] = static_cast<uint8_t>(lane);
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the table reads below after its writes (one wave: LDS in order)
+  const bool work = static_cast<uint32_t>(lane) < total;
+  const int src = work ? static_cast<int>(otab[lane]) : lane;
+  // the owner's ray and closest hit of the trip start; p = owner's first + (lane - owner's pre)
+  const int base = bperm_i(src, first - static_cast<int>(pre));
+  const V3 wo = v3(bperm_f(src, o.x), bperm_f(src, o.y), bperm_f(src, o.z));
+  const V3 wd = v3(bperm_f(src, d.x), bperm_f(src, d.y), bperm_f(src, d.z));
+  // a = d.d and its reciprocal recomputed from the owner's d as trav_begin formed them (bit-identical)
+  const float wa = dot(wd, wd), winv = div_rn(1.0f, wa), wtime = bperm_f(src, time);
+  const int worigin = bperm_i(src, t.origin);
+  float th = -1.0f;
+  int32_t wm = 0;
+  if (work) {
+    const int32_t p = base + lane;
+    const float4* sp4 = S.spheres + static_cast<int64_t>(p) * S.sphere_f4;
+    if (COUNT) cnt.prim += 1;
+    // tmax = +inf instead of the owner's tbest: a root past tbest is returned here and rejected by the
+    // owner (r < t.tbest), where the bounded test returned -1 or the same root — the same outcome
+    th = sphere_t<true>(sp4[0], sp4[1], wo, wd, wa, winv, wtime, kTMin, __builtin_inff(), p == worigin);
+    if (MAT) wm = ibits(sp4[1].w);
+  }
+  // owners: the roots in leaf order, as the one-at-a-time walk applies them
+  for (int j = 0; j < 8; ++j) {
+    const bool mine = j < n && pre + j < 64u;
+    if (ballot(mine) == 0) break;
+    const int from = mine ? static_cast<int>(pre) + j : lane;
+    const float r = bperm_f(from, th);
+    const int32_t rm = MAT ? bperm_i(from, wm) : 0;
+    if (mine) {
+      bool take = r > 0.0f && r < t.tbest;
+      if (ballot_tie(r == t.tbest) != 0 && r == t.tbest) {
+        const int32_t* rk = tie_ranks_at_tie<COUNT>(S, corrupt);
+        take = rk[first + j] < rk[t.best];
+      }
+      if (take) {
+        t.tbest = r;
+        t.best = first + j;
+        t.mat = MAT ? rm : -1;
+      }
+    }
+  }
+  if (n > 0) {
+    const int done = min(n, max(0, 64 - static_cast<int>(pre)));
+    if (done == n) {
+      trav_pop(t, stk);
+    } else if (done > 0) {
+      t.todo = ~(((first + done) << 3) | (n - done - 1));
+    }
+  }
+}
+
 // A lane's pixel, packed: column in the low 16 bits, shard-local row in the high 16 bits.
 __device__ __forceinline__ int px_i(uint32_t px) { return static_cast<int>(px & 0xffffu); }
 __device__ __forceinline__ int px_lr(uint32_t px) { return static_cast<int>(px >> 16); }
@@ -1183,7 +1285,7 @@ __device__ __forceinline__ void ring_batch_done(__amdgpu_buffer_rsrc_t rs, const
 // closest-hit query, and lanes still traversing keep their stack and continue afterwards.
 template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM, bool RING, int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                              const Stk& stk, WaveStats<COUNT>& w, lu32* rtab) {
+                                              const Stk& stk, WaveStats<COUNT>& w, lu32* rtab, lu8* otab) {
   const int lane = __lane_id();
   const bool no_work = C.max_depth <= 0 || C.spp <= 0;  // every pixel is black (camera.hpp:192)
   const int num_batches = J.num_tiles * J.chunks;
@@ -1377,9 +1479,16 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           w.diag[9] += __popcll(ballot(at_inner(tr)));
         }
       }
-      if (leaf_trip && tr.todo < 0)
+      // sphere-only scenes: the leaf trip's pairs spread over the wave (leaf_pairs; RTG_LEAF_PAIRS=0 builds
+      // the one-sphere-per-lane trip for A/B)
+      constexpr bool kPairs = RTG_LEAF_PAIRS && (PRIMS & kPrimsKind) == kPrimsSpheres && WIDE == 4;
+      if constexpr (kPairs) {
+        if (leaf_trip) leaf_pairs<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk,
+                                                                                  w.cnt, w.corrupt, otab);
+      } else if (leaf_trip && tr.todo < 0) {
         leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM, PRIMS, GEOM == kGeomLds || !RING>(
             tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
+      }
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
@@ -1475,9 +1584,9 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   if constexpr (SPILL) {
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, stk, w, rtab);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, stk, w, rtab, nullptr);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, LdsStack<STACK>{lstk}, w, rtab);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, LdsStack<STACK>{lstk}, w, rtab, nullptr);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, slot, (blockIdx.x << 8) | wave);
@@ -1487,7 +1596,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCamera& C, const DevJob& J,
                                                  unsigned char* smem, int kFill, int wpb, uint64_t t0, int lane,
-                                                 int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab) {
+                                                 int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab, lu8* otab) {
   // the whole-scene LDS schedule of 4-wide trees without a stack spill and without image / noise
   // textures keeps 16-bit stack entries (the LDS room that lets book-1 run the dual launch; the
   // textured kernels keep 32-bit ones: earth_perlin +2 % with 16-bit)
@@ -1557,12 +1666,12 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
     const int slot = blockIdx.x * wpb + wave;
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, stk, w, rtab);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, stk, w, rtab, otab);
   } else if constexpr (STK16) {
     render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack16<STACK>{lstk16}, w,
-                                                                             rtab);
+                                                                             rtab, otab);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w, rtab, otab);
   }
   flush_stats<COUNT>(J, w, lane);
   trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
@@ -1597,6 +1706,7 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
   lu32* rtab = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_ring)) +
                (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
+  lu8* otab = (lu8*)(smem + J.lds_pairs) + __builtin_amdgcn_readfirstlane(wave) * 64;  // leaf_pairs' owner table
   if constexpr (GEOM == kGeomTreelet) {
     float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
     for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += kFill) l_top[k] = S.nodes[k];
@@ -1613,16 +1723,16 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
       int32_t* tstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * J.lds_stack * 64 + lane;
       const SpillStack<STACK> stk{tstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                   J.lds_stack, J.lds_stack + J.spill_depth};
-      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, stk, w, rtab);
+      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, stk, w, rtab, otab);
     } else {
       render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w,
-                                                                                rtab);
+                                                                                rtab, otab);
     }
     flush_stats<COUNT>(J, w, lane);
     trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
   } else {
     render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, PRIMS>(S, C, J, smem, kFill, wpb, t0, lane, wave,
-                                                                          lstk, lstk16, rtab);
+                                                                          lstk, lstk16, rtab, otab);
   }
 }
 
@@ -1813,6 +1923,8 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   off = a16(off + int64_t(S.num_perlins) * 768 * 4);
   const int64_t ring = off;  // RING kernels (J->ring_log2 >= 0): per-wave batch tables
   if (J && J->ring_log2 >= 0) off += int64_t(waves) * kRingEntries * 4;
+  const int64_t pairs = off;  // sphere-only kernels: leaf_pairs' 64-byte owner table per wave
+  if (RTG_LEAF_PAIRS && S.ref_mode == 1) off = a16(off + int64_t(waves) * 64);
   if (off > 160 * 1024) return -1;
   if (J) {
     J->lds_materials = static_cast<int32_t>(materials);
@@ -1825,6 +1937,7 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
     J->lds_perlin_vec = static_cast<int32_t>(pvec);
     J->lds_perlin_perm = static_cast<int32_t>(pperm);
     J->lds_ring = static_cast<int32_t>(ring);
+    J->lds_pairs = static_cast<int32_t>(pairs);
   }
   return static_cast<int>(off);
 }
@@ -1834,15 +1947,18 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
   const int64_t stacks = int64_t(waves) * stack * 64 * 4;
   const int64_t ring = J->ring_log2 >= 0 ? int64_t(waves) * kRingEntries * 4 : 0;  // RING: batch tables
-  const int64_t room = 160 * 1024 - stacks - ring;
+  // sphere-only kernels: leaf_pairs' 64-byte owner table per wave
+  const int64_t pairs = RTG_LEAF_PAIRS && S->ref_mode == 1 && S->tex_full == 0 ? int64_t(waves) * 64 : 0;
+  const int64_t room = 160 * 1024 - stacks - ring - pairs;
   const int64_t nb = node_bytes(S->node_width);
   if (S->node_width < 4 || room < nb) return -1;
   const int64_t nodes = std::min<int64_t>(S->num_nodes, room / nb);
   S->treelet_bytes = static_cast<int32_t>(nodes * nb);
   J->lds_ring = static_cast<int32_t>(stacks);
-  J->lds_nodes = static_cast<int32_t>(stacks + ring);
+  J->lds_pairs = static_cast<int32_t>(stacks + ring);
+  J->lds_nodes = static_cast<int32_t>(stacks + ring + pairs);
   J->lds_stacks = 0;
-  return static_cast<int>(stacks + ring + nodes * nb);
+  return static_cast<int>(stacks + ring + pairs + nodes * nb);
 }
 
 // The dual launch (rtg_api.cpp) needs the 16-wave workgroup's four waves and the 4-wave workgroup's

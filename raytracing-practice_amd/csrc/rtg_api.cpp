@@ -1519,7 +1519,9 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     P->ring_slots = 1 << lg;
     P->ring_bytes = (static_cast<size_t>(dj.chunks) << (lg + 10)) + (size_t(8) << lg);
   }
-  P->skip_kernel = P->progressive && dc.max_depth <= 0;  // every chunk sum is black
+  // max_depth <= 0: every pixel is black and nothing is traced (camera.hpp:183-186): no kernel; the frame
+  // (one-shot) or the chunk sums (progressive) are zeroed by rtg_render
+  P->skip_kernel = dc.max_depth <= 0;
   if (P->skip_kernel || variant != 3) lds4 = -1;
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
@@ -1861,10 +1863,11 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     if ((pst = grow(s->scr_partial, out_bytes * dj.chunks, "hipMalloc(partial sums)")) != RTG_OK) return pst;
     dj.partial = static_cast<float*>(s->scr_partial.p);
   }
-  if (P.skip_kernel)
+  if (P.skip_kernel && P.progressive)
     RTG_HIP(hipMemsetAsync(dj.partial + static_cast<size_t>(dj.chunk_begin) * rows * W * 3, 0,
                            out_bytes * dj.chunks, stream),
             "hipMemsetAsync(partial sums)");
+  if (P.skip_kernel && !P.progressive && dout) RTG_HIP(hipMemsetAsync(dout, 0, out_bytes, stream), "hipMemsetAsync(out)");
   RTG_HIP(hipEventRecord(s->ev0, stream), "hipEventRecord");
   const int lds4 = P.lds4;
   if (K.verbose)
@@ -1898,7 +1901,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     RTG_HIP(hipEventRecord(s->ev_join, s->aux_stream), "hipEventRecord");
     RTG_HIP(hipStreamWaitEvent(stream, s->ev_join, 0), "hipStreamWaitEvent");
   }
-  if ((P.chunked && !P.ring_slots) || (P.progressive && dout))
+  if ((P.chunked && !P.ring_slots && !(P.skip_kernel && !P.progressive)) || (P.progressive && dout))
     RTG_HIP(launch_combine(dj.partial, dout, static_cast<int64_t>(rows) * W, P.sum_chunks, P.out_scale, stream),
             "combine kernel launch");
   RTG_HIP(hipEventRecord(s->ev1, stream), "hipEventRecord");

@@ -821,8 +821,12 @@ __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3
       if (img < 0) return v3(0.0f, 1.0f, 1.0f);
       const int4 h = S.images[img];
       if (h.y <= 0) return v3(0.0f, 1.0f, 1.0f);
+      // the empty asm keeps v's flip here: hoisted out of the nesting loop (it is loop-invariant), 1 - v
+      // outlived the loop in scratch (config 3's textured kernel, round 6)
+      float vin = v;
+      __asm__ volatile("" : "+v"(vin));
       const float uc = fminf(fmaxf(u, 0.0f), 1.0f);
-      const float vc = 1.0f - fminf(fmaxf(v, 0.0f), 1.0f);
+      const float vc = 1.0f - fminf(fmaxf(vin, 0.0f), 1.0f);
       int i = static_cast<int>(uc * static_cast<float>(h.x));
       int j = static_cast<int>(vc * static_cast<float>(h.y));
       i = i < 0 ? 0 : (i < h.x ? i : h.x - 1);
@@ -1001,6 +1005,14 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
+// The lane id recomputed where a kernel ends (flush_stats, trace_wave): an asm mbcnt the compiler cannot merge
+// with the one at the kernel's start, so the lane id is not held (or spilled, config 3) across the render loop
+__device__ __forceinline__ int lane_now() {
+  int l;
+  __asm__ volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // Per-wave accumulators that outlive one tile.
 template <bool COUNT>
 struct WaveStats {
@@ -1063,8 +1075,9 @@ __device__ __forceinline__ int bperm_i(int src, int v) { return __builtin_amdgcn
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
 }
+// Returns the lanes that tested a sphere (wave-uniform; the COUNT diagnostics' leaf-trip lanes).
 template <class Stk, bool COUNT, bool CHECK, bool MAT>
-__device__ __forceinline__ void leaf_pairs(Trav& t, const DevScene& S, V3 o, V3 d, float time, const Stk& stk,
+__device__ __forceinline__ int leaf_pairs(Trav& t, const DevScene& S, V3 o, V3 d, float time, const Stk& stk,
                                            Counts<COUNT>& cnt, bool& corrupt, lu8* otab) {
   const int lane = __lane_id();
   int32_t first = 0, n = 0;
@@ -1139,6 +1152,7 @@ __device__ __forceinline__ void leaf_pairs(Trav& t, const DevScene& S, V3 o, V3 
       t.todo = ~(((first + done) << 3) | (n - done - 1));
     }
   }
+  return static_cast<int>(min(total, 64u));
 }
 
 // A lane's pixel, packed: column in the low 16 bits, shard-local row in the high 16 bits.
@@ -1287,7 +1301,10 @@ template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM, bool RING, int P
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
                                               const Stk& stk, WaveStats<COUNT>& w, lu32* rtab, lu8* otab) {
   const int lane = __lane_id();
-  const bool no_work = C.max_depth <= 0 || C.spp <= 0;  // every pixel is black (camera.hpp:192)
+  // max_depth <= 0: every pixel is black and no segment is traced (camera.hpp:183-186); rtg_render writes
+  // that frame itself and launches nothing (round 6: the hand-out loop no longer carries a branch for it,
+  // whose zero triple the textured kernel kept in scratch), so this exit is only a guard
+  if (C.max_depth <= 0 || C.spp <= 0) return;
   const int num_batches = J.num_tiles * J.chunks;
   V3 acc = v3(0.0f, 0.0f, 0.0f);
   uint32_t px = 0;
@@ -1394,20 +1411,13 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         const int lr = by + (k >> J.tile_lw);
         if (i < C.width && lr < J.row_count) {
           px = static_cast<uint32_t>(i) | (static_cast<uint32_t>(lr) << 16);
-          if (no_work) {
-            if (bc == 0) {
-              float* o = J.out + (static_cast<int64_t>(lr) * C.width + i) * 3;
-              o[0] = o[1] = o[2] = 0.0f;
-            }
-          } else {
-            fresh = true;
-            chunk = ring ? ((((cur_tile() & ((1 << J.ring_log2) - 1)) * J.chunks + (bc - J.chunk_begin)) << 6) + k) |
-                               (cur_e << 28)
-                         : bc;
-            sample = bc * J.chunk_samples;
-            s_end = min(sample + J.chunk_samples, C.spp);
-            acc = v3(0.0f, 0.0f, 0.0f);
-          }
+          fresh = true;
+          chunk = ring ? ((((cur_tile() & ((1 << J.ring_log2) - 1)) * J.chunks + (bc - J.chunk_begin)) << 6) + k) |
+                             (cur_e << 28)
+                       : bc;
+          sample = bc * J.chunk_samples;
+          s_end = min(sample + J.chunk_samples, C.spp);
+          acc = v3(0.0f, 0.0f, 0.0f);
         } else {
           outside = true;
         }
@@ -1483,8 +1493,11 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       // the one-sphere-per-lane trip for A/B)
       constexpr bool kPairs = RTG_LEAF_PAIRS && (PRIMS & kPrimsKind) == kPrimsSpheres && WIDE == 4;
       if constexpr (kPairs) {
-        if (leaf_trip) leaf_pairs<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time, stk,
-                                                                                  w.cnt, w.corrupt, otab);
+        if (leaf_trip) {
+          const int workers = leaf_pairs<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time,
+                                                                                         stk, w.cnt, w.corrupt, otab);
+          if (COUNT) w.diag[10] += workers - at_leaf;  // lanes testing a sphere, not lanes at a leaf
+        }
       } else if (leaf_trip && tr.todo < 0) {
         leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM, PRIMS, GEOM == kGeomLds || !RING>(
             tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
@@ -1588,8 +1601,8 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   } else {
     render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, LdsStack<STACK>{lstk}, w, rtab, nullptr);
   }
-  flush_stats<COUNT>(J, w, lane);
-  trace_wave(J, t0, w.pixels, lane, slot, (blockIdx.x << 8) | wave);
+  flush_stats<COUNT>(J, w, lane_now());
+  trace_wave(J, t0, w.pixels, lane_now(), slot, (blockIdx.x << 8) | wave);
 }
 
 // Schedule 3's body: the whole scene in the workgroup's LDS (render_kernel_lds with GEOM = kGeomLds).
@@ -1673,8 +1686,8 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
   } else {
     render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w, rtab, otab);
   }
-  flush_stats<COUNT>(J, w, lane);
-  trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
+  flush_stats<COUNT>(J, w, lane_now());
+  trace_wave(J, t0, w.pixels, lane_now(), blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
 }
 
 // Schedule 3 (default when the geometry fits): persistent workgroups of WAVES waves, one per CU.
@@ -1728,8 +1741,8 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
       render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w,
                                                                                 rtab, otab);
     }
-    flush_stats<COUNT>(J, w, lane);
-    trace_wave(J, t0, w.pixels, lane, blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
+    flush_stats<COUNT>(J, w, lane_now());
+    trace_wave(J, t0, w.pixels, lane_now(), blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
   } else {
     render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, PRIMS>(S, C, J, smem, kFill, wpb, t0, lane, wave,
                                                                           lstk, lstk16, rtab, otab);

@@ -515,8 +515,8 @@ def test_progressive_chunks_and_checkpoint(gpu_lib, scenes):
     ds.close()
 
 
-@pytest.mark.parametrize("case", ["one_pixel", "odd_width", "depth0", "depth1", "spp1", "pinhole",
-                                  "tall"])
+@pytest.mark.parametrize("case", ["one_pixel", "odd_width", "depth0", "depth0_chunked", "depth1", "spp1",
+                                  "pinhole", "tall"])
 def test_edge_cases(gpu_lib, scenes, oracle, case):
     kw = dict(image_width=33, samples_per_pixel=3, max_depth=10)
     if case == "one_pixel":
@@ -525,6 +525,8 @@ def test_edge_cases(gpu_lib, scenes, oracle, case):
         kw.update(image_width=17, aspect_ratio=17 / 5)
     elif case == "depth0":
         kw.update(max_depth=0)
+    elif case == "depth0_chunked":  # black frame written by rtg_render (no kernel), 3 sample chunks
+        kw.update(max_depth=0, samples_per_pixel=40)
     elif case == "depth1":
         kw.update(max_depth=1)
     elif case == "spp1":
@@ -535,7 +537,7 @@ def test_edge_cases(gpu_lib, scenes, oracle, case):
         kw.update(image_width=9, aspect_ratio=0.25)
     g, o, st, segs = compare(gpu_lib, scenes, oracle, "bouncing_spheres", **kw)
     assert_parity(g, o, st, segs)
-    if case == "depth0":
+    if case.startswith("depth0"):
         assert st.segments == 0 and not g.any()
 
 

@@ -320,7 +320,7 @@ Knobs read_knobs() {
   };
   k.verbose = std::getenv("RTG_VERBOSE") != nullptr;
   num("RTG_TILE_LW", 0, 6, &k.tile_lw);
-  num("RTG_CHUNK_SAMPLES", 1, 1 << 20, &k.chunk_samples);
+  num("RTG_CHUNK_SAMPLES", 1, 63, &k.chunk_samples);  // <= 63: the kernels pack a unit's samples left in 6 bits
   num("RTG_STACK_LDS_ENTRIES", 1, 32, &k.stack_lds_entries);
   int w = 0;
   if (num("RTG_LDS_WAVES", 4, 16, &w) && (w == 4 || w == 16)) k.lds_waves = w;
@@ -1352,6 +1352,8 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     dj.tiles_x = (W + tw - 1) / tw;
     dj.num_tiles = dj.tiles_x * ((rows + th - 1) / th);
   }
+  // the kernels pack a lane's sample index in 26 bits (render_stream's `su`)
+  if (cam->samples_per_pixel >= (1 << 26)) return fail(RTG_E_UNSUPPORTED, "samples_per_pixel must be below 2^26");
   dj.chunk_samples = rtg_chunk_samples(cam->samples_per_pixel);
   // RTG_CHUNK_SAMPLES overrides K for schedule experiments (the frame then differs from the spec)
   if (K.chunk_samples > 0) dj.chunk_samples = K.chunk_samples;
@@ -1525,15 +1527,13 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
   if (P->skip_kernel || variant != 3) lds4 = -1;
   if (lds4 > 0) {  // the dual launch's job: the same frame, counters and buffers as dj
     const int32_t l4[] = {j4.lds_nodes, j4.lds_refs, j4.lds_spheres, j4.lds_quads, j4.lds_materials,
-                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks, j4.lds_ring,
-                          j4.lds_pairs};
+                          j4.lds_textures, j4.lds_perlin_vec, j4.lds_perlin_perm, j4.lds_stacks, j4.lds_ring};
     j4 = dj;
     j4.lds_waves = 4;
     j4.lds_nodes = l4[0], j4.lds_refs = l4[1], j4.lds_spheres = l4[2], j4.lds_quads = l4[3];
     j4.lds_materials = l4[4], j4.lds_textures = l4[5], j4.lds_perlin_vec = l4[6], j4.lds_perlin_perm = l4[7];
     j4.lds_stacks = l4[8];
     j4.lds_ring = l4[9];
-    j4.lds_pairs = l4[10];
     j4.trace = nullptr;  // the per-wave timeline covers the main launch's waves only
   }
   P->j4 = j4;

@@ -302,7 +302,6 @@ struct DevJob {
   int32_t stack_esz;                         // persistent kernels: bytes per LDS stack entry (2 or 4)
   int32_t lds_stacks;                        // persistent kernels: byte offset of the traversal stacks in LDS
   int32_t lds_ring;                          // RING kernels: byte offset of the per-wave batch tables (64 B each)
-  int32_t lds_pairs;                         // sphere-only kernels: byte offset of leaf_pairs' owner tables (64 B per wave)
 };
 
 }  // namespace rtg

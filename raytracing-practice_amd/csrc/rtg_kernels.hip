@@ -32,11 +32,6 @@
 namespace rtg {
 namespace {
 
-// leaf trips of sphere-only scenes spread their (ray, sphere) pairs over the wave (leaf_pairs); 0 builds the
-// one-sphere-per-lane trip (A/B)
-#ifndef RTG_LEAF_PAIRS
-#define RTG_LEAF_PAIRS 1
-#endif
 constexpr float kTMin = 0.001f;  // interval(0.001, infinity), camera.hpp:192
 // Conservative culling. Box tests only prune: a child is skipped when
 // its entry distance is past fmaf(tbest, kCullRel, kCullAbs) or its exit before kCullTMin, a margin at
@@ -946,6 +941,12 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
   V3 dir, att;
   constexpr bool kDiffuse = (PRIMS & kPrimsDiffuse) != 0;
   if (type == RTG_MAT_LAMBERTIAN || (!kDiffuse && type == RTG_MAT_METAL)) {
+    // the albedo first (it draws no random numbers): with the direction drawn first, one of its uniforms
+    // stayed live across the texture evaluation and went to scratch in the textured kernel (round 6)
+    if (kDiffuse || type == RTG_MAT_LAMBERTIAN) {
+      if (needs_uv) sphere_uv();
+      att = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);
+    }
     // both scatter around a random unit vector: one sampling code path for the lanes of either
     const V3 r = random_unit_vector(ps.rng);
     if (kDiffuse || type == RTG_MAT_LAMBERTIAN) {
@@ -953,8 +954,6 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
       // near_zero with the reference's fabs(e[1] < s) quirk (vec3.hpp:70-77, H5)
       const float s = 1e-8f;
       if (fabsf(dir.x) < s && dir.y < s && fabsf(dir.z) < s) dir = n;
-      if (needs_uv) sphere_uv();
-      att = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);
     } else {
       const V3 in = ps.d;
       const V3 refl = madd(-(2.0f * dot(in, n)), n, in);
@@ -1054,105 +1053,6 @@ __device__ __forceinline__ void flush_stats(const DevJob& J, WaveStats<COUNT>& w
   if (lane == 0) atomicAdd(&J.counters[0], static_cast<unsigned long long>(wsegs));
   if (__any(w.overflow) && lane == 0) atomicAdd(&J.counters[4], 1ull);
   if (__any(w.corrupt) && lane == 0) atomicAdd(&J.counters[5], 1ull);
-}
-
-// Leaf trip with the leaf lanes' (ray, sphere) pairs spread over the whole wave (VERDICT r05 items 2-3;
-// sphere-only scenes, whose leaf refs are the identity). In a leaf trip only the lanes waiting at a leaf
-// (about a third of the wave on book-1 and the 1M field) test a sphere, one per trip, and a leaf of n
-// spheres costs its lane n trips. Here every pending pair of the trip gets a lane of its own: the leaf
-// lanes' counts are prefix-summed (bit planes of n through ballot + mbcnt), each owner writes its lane id
-// into the wave's 64-byte owner table (LDS) at its pair slots [pre, pre + n), every lane below the total
-// reads its owner there and fetches the owner's ray with ds_bpermute, tests its sphere (unbounded above),
-// and each owner reads its pairs' roots back in leaf order and applies them as the one-at-a-time walk
-// would (a root past the owner's current tbest is a miss there too, and the exact-t tie rule compares the
-// same roots in the same order), so frames are those of leaf_step. Pairs past the
-// 64th stay with their owner (its leaf code advanced) for the next leaf trip. Called by the whole wave.
-typedef __attribute__((address_space(3))) uint8_t lu8;
-__device__ __forceinline__ float bperm_f(int src, float v) {
-  return __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(v)));
-}
-__device__ __forceinline__ int bperm_i(int src, int v) { return __builtin_amdgcn_ds_bpermute(src << 2, v); }
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
-}
-// Returns the lanes that tested a sphere (wave-uniform; the COUNT diagnostics' leaf-trip lanes).
-template <class Stk, bool COUNT, bool CHECK, bool MAT>
-__device__ __forceinline__ int leaf_pairs(Trav& t, const DevScene& S, V3 o, V3 d, float time, const Stk& stk,
-                                           Counts<COUNT>& cnt, bool& corrupt, lu8* otab) {
-  const int lane = __lane_id();
-  int32_t first = 0, n = 0;
-  if (t.todo < 0) {
-    const int32_t code = ~t.todo;
-    first = code >> 3;
-    n = (code & 7) + 1;
-    if ((CHECK || COUNT) && static_cast<int64_t>(first) + n > S.num_refs) {
-      corrupt = true;
-      t.todo = kTravDone;
-      n = 0;
-    }
-  }
-  // exclusive prefix of n over the lanes, and the trip's pair total, from n's four bit planes (n <= 8)
-  uint32_t pre = 0, total = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const uint64_t m = ballot(((n >> b) & 1) != 0);
-    pre += lanes_below(m) << b;
-    total += static_cast<uint32_t>(__popcll(m)) << b;
-  }
-  for (int j = 0; j < 8; ++j) {
-    if (ballot(j < n && pre + j < 64u) == 0) break;
-    if (j < n && pre + j < 64u) otab[pre + j] = static_cast<uint8_t>(lane);
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the table reads below after its writes (one wave: LDS in order)
-  const bool work = static_cast<uint32_t>(lane) < total;
-  const int src = work ? static_cast<int>(otab[lane]) : lane;
-  // the owner's ray and closest hit of the trip start; p = owner's first + (lane - owner's pre)
-  const int base = bperm_i(src, first - static_cast<int>(pre));
-  const V3 wo = v3(bperm_f(src, o.x), bperm_f(src, o.y), bperm_f(src, o.z));
-  const V3 wd = v3(bperm_f(src, d.x), bperm_f(src, d.y), bperm_f(src, d.z));
-  // a = d.d and its reciprocal recomputed from the owner's d as trav_begin formed them (bit-identical)
-  const float wa = dot(wd, wd), winv = div_rn(1.0f, wa), wtime = bperm_f(src, time);
-  const int worigin = bperm_i(src, t.origin);
-  float th = -1.0f;
-  int32_t wm = 0;
-  if (work) {
-    const int32_t p = base + lane;
-    const float4* sp4 = S.spheres + static_cast<int64_t>(p) * S.sphere_f4;
-    if (COUNT) cnt.prim += 1;
-    // tmax = +inf instead of the owner's tbest: a root past tbest is returned here and rejected by the
-    // owner (r < t.tbest), where the bounded test returned -1 or the same root — the same outcome
-    th = sphere_t<true>(sp4[0], sp4[1], wo, wd, wa, winv, wtime, kTMin, __builtin_inff(), p == worigin);
-    if (MAT) wm = ibits(sp4[1].w);
-  }
-  // owners: the roots in leaf order, as the one-at-a-time walk applies them
-  for (int j = 0; j < 8; ++j) {
-    const bool mine = j < n && pre + j < 64u;
-    if (ballot(mine) == 0) break;
-    const int from = mine ? static_cast<int>(pre) + j : lane;
-    const float r = bperm_f(from, th);
-    const int32_t rm = MAT ? bperm_i(from, wm) : 0;
-    if (mine) {
-      bool take = r > 0.0f && r < t.tbest;
-      if (ballot_tie(r == t.tbest) != 0 && r == t.tbest) {
-        const int32_t* rk = tie_ranks_at_tie<COUNT>(S, corrupt);
-        take = rk[first + j] < rk[t.best];
-      }
-      if (take) {
-        t.tbest = r;
-        t.best = first + j;
-        t.mat = MAT ? rm : -1;
-      }
-    }
-  }
-  if (n > 0) {
-    const int done = min(n, max(0, 64 - static_cast<int>(pre)));
-    if (done == n) {
-      trav_pop(t, stk);
-    } else if (done > 0) {
-      t.todo = ~(((first + done) << 3) | (n - done - 1));
-    }
-  }
-  return static_cast<int>(min(total, 64u));
 }
 
 // A lane's pixel, packed: column in the low 16 bits, shard-local row in the high 16 bits.
@@ -1299,7 +1199,7 @@ __device__ __forceinline__ void ring_batch_done(__amdgpu_buffer_rsrc_t rs, const
 // closest-hit query, and lanes still traversing keep their stack and continue afterwards.
 template <class Stk, bool COUNT, int WIDE, bool TEXF, int GEOM, bool RING, int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera& C, const DevJob& J,
-                                              const Stk& stk, WaveStats<COUNT>& w, lu32* rtab, lu8* otab) {
+                                              const Stk& stk, WaveStats<COUNT>& w, lu32* rtab) {
   const int lane = __lane_id();
   // max_depth <= 0: every pixel is black and no segment is traced (camera.hpp:183-186); rtg_render writes
   // that frame itself and launches nothing (round 6: the hand-out loop no longer carries a branch for it,
@@ -1308,11 +1208,15 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   const int num_batches = J.num_tiles * J.chunks;
   V3 acc = v3(0.0f, 0.0f, 0.0f);
   uint32_t px = 0;
-  // s_end: end of the lane's unit (0: the lane holds no unit; an integer, not a bool, for the same
-  // reason as kTravDone: ballots of it need no lane-mask copy)
-  int sample = 0, s_end = 0, chunk = 0;
-  auto has = [&]() { return s_end != 0; };
-  // fresh: the lane starts sample `sample` of its unit at the top of the next loop trip (the one
+  // su: the lane's unit, its current sample index in bits 0-25 and the samples it has left (1 .. 63) in bits
+  // 26-31; 0: the lane holds no unit (an integer, not a bool, for the same reason as kTravDone: ballots of
+  // it need no lane-mask copy). One register for the sample and the unit's end (round 6: the 96-VGPR
+  // kernels had none to spare; the host keeps spp < 2^26 and K <= 63)
+  constexpr uint32_t kSampleBits = 26, kSampleMask = (1u << kSampleBits) - 1u;
+  uint32_t su = 0;
+  int chunk = 0;
+  auto has = [&]() { return su != 0; };
+  // fresh: the lane starts sample (su & kSampleMask) of its unit at the top of the next loop trip (the one
   // start path for the next sample of a unit and the first sample of a new unit); cont: its path
   // continues with a new segment (ps.o / ps.d scattered)
   bool fresh = false, cont = false;
@@ -1415,8 +1319,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           chunk = ring ? ((((cur_tile() & ((1 << J.ring_log2) - 1)) * J.chunks + (bc - J.chunk_begin)) << 6) + k) |
                              (cur_e << 28)
                        : bc;
-          sample = bc * J.chunk_samples;
-          s_end = min(sample + J.chunk_samples, C.spp);
+          const int s0 = bc * J.chunk_samples;
+          su = (static_cast<uint32_t>(min(s0 + J.chunk_samples, C.spp) - s0) << kSampleBits) | static_cast<uint32_t>(s0);
           acc = v3(0.0f, 0.0f, 0.0f);
         } else {
           outside = true;
@@ -1432,7 +1336,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
     }
     uint64_t t_start = 0;
     if (COUNT) t_start = __builtin_amdgcn_s_memtime();
-    if (fresh) start_pixel_sample(ps, C, J, px, static_cast<uint32_t>(sample));
+    if (fresh) start_pixel_sample(ps, C, J, px, su & kSampleMask);
     if (COUNT) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       w.diag[13] += t_start - t_top;  // unit hand-out
@@ -1489,19 +1393,9 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           w.diag[9] += __popcll(ballot(at_inner(tr)));
         }
       }
-      // sphere-only scenes: the leaf trip's pairs spread over the wave (leaf_pairs; RTG_LEAF_PAIRS=0 builds
-      // the one-sphere-per-lane trip for A/B)
-      constexpr bool kPairs = RTG_LEAF_PAIRS && (PRIMS & kPrimsKind) == kPrimsSpheres && WIDE == 4;
-      if constexpr (kPairs) {
-        if (leaf_trip) {
-          const int workers = leaf_pairs<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds>(tr, S, ps.o, ps.d, ps.time,
-                                                                                         stk, w.cnt, w.corrupt, otab);
-          if (COUNT) w.diag[10] += workers - at_leaf;  // lanes testing a sphere, not lanes at a leaf
-        }
-      } else if (leaf_trip && tr.todo < 0) {
+      if (leaf_trip && tr.todo < 0)
         leaf_step<Stk, COUNT, GEOM != kGeomLds, GEOM != kGeomLds, WIDE, GEOM, PRIMS, GEOM == kGeomLds || !RING>(
             tr, S, ps.o, ps.d, ps.time, stk, w.cnt, w.corrupt);
-      }
       // lanes at inner nodes step in every trip: in a leaf trip they would otherwise idle, and the
       // node step's LDS latency overlaps the primitive tests (measured -3% on book-1, -7% Cornell)
       // node steps per trip: 2 where nodes come through the caches (config 5 -2.1 %: half the trip
@@ -1550,8 +1444,8 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
       cont = alive_path;
       if (!alive_path) {
         acc = add(acc, ps.L);
-        ++sample;
-        if (sample < s_end) {
+        su += 1u - (1u << kSampleBits);  // the next sample, one fewer left
+        if ((su >> kSampleBits) != 0) {
           fresh = true;
         } else {
           const int64_t pix = static_cast<int64_t>(px_lr(px)) * C.width + px_i(px);
@@ -1569,7 +1463,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
             o[1] = acc.y;
             o[2] = acc.z;
           }
-          s_end = 0;  // the unit is done
+          su = 0;  // the unit is done
           ++w.pixels;
         }
       }
@@ -1588,7 +1482,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   __shared__ int32_t s_stack[4 * STACK * 64];
   __shared__ uint32_t s_ring[RING ? 4 * kRingEntries : 1];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: an SGPR, not a VGPR held (or spilled) across the render loop
   const int slot = blockIdx.x * 4 + wave;
   lu32* rtab = (lu32*)(s_ring) + (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
   int32_t* lstk = s_stack + wave * STACK * 64 + lane;
@@ -1597,9 +1491,9 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
   if constexpr (SPILL) {
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, stk, w, rtab, nullptr);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, stk, w, rtab);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, LdsStack<STACK>{lstk}, w, rtab, nullptr);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomGlobal, RING>(S, C, J, LdsStack<STACK>{lstk}, w, rtab);
   }
   flush_stats<COUNT>(J, w, lane_now());
   trace_wave(J, t0, w.pixels, lane_now(), slot, (blockIdx.x << 8) | wave);
@@ -1609,7 +1503,7 @@ __global__ __launch_bounds__(256) void render_kernel(DevScene S, DevCamera C, De
 template <int STACK, bool SPILL, bool COUNT, int WAVES, int WIDE, bool TEXF, bool RING, int PRIMS = kPrimsAny>
 __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCamera& C, const DevJob& J,
                                                  unsigned char* smem, int kFill, int wpb, uint64_t t0, int lane,
-                                                 int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab, lu8* otab) {
+                                                 int wave, int32_t* lstk, int16_t* lstk16, lu32* rtab) {
   // the whole-scene LDS schedule of 4-wide trees without a stack spill and without image / noise
   // textures keeps 16-bit stack entries (the LDS room that lets book-1 run the dual launch; the
   // textured kernels keep 32-bit ones: earth_perlin +2 % with 16-bit)
@@ -1679,12 +1573,12 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
     const int slot = blockIdx.x * wpb + wave;
     const SpillStack<STACK> stk{lstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                 J.lds_stack, J.lds_stack + J.spill_depth};
-    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, stk, w, rtab, otab);
+    render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, stk, w, rtab);
   } else if constexpr (STK16) {
     render_stream<LdsStack16<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack16<STACK>{lstk16}, w,
-                                                                             rtab, otab);
+                                                                             rtab);
   } else {
-    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w, rtab, otab);
+    render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomLds, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w, rtab);
   }
   flush_stats<COUNT>(J, w, lane_now());
   trace_wave(J, t0, w.pixels, lane_now(), blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
@@ -1714,12 +1608,11 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: an SGPR, not a VGPR held (or spilled) across the render loop
   int32_t* lstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
   int16_t* lstk16 = reinterpret_cast<int16_t*>(smem + J.lds_stacks) + wave * STACK * 64 + lane;
   lu32* rtab = (lu32*)(reinterpret_cast<uint32_t*>(smem + J.lds_ring)) +
                (RING ? __builtin_amdgcn_readfirstlane(wave) * kRingEntries : 0);
-  lu8* otab = (lu8*)(smem + J.lds_pairs) + __builtin_amdgcn_readfirstlane(wave) * 64;  // leaf_pairs' owner table
   if constexpr (GEOM == kGeomTreelet) {
     float4* l_top = reinterpret_cast<float4*>(smem + J.lds_nodes);
     for (int k = threadIdx.x; k < S.treelet_bytes / 16; k += kFill) l_top[k] = S.nodes[k];
@@ -1736,16 +1629,16 @@ void render_kernel_lds(DevScene S, DevCamera C, DevJob J) {
       int32_t* tstk = reinterpret_cast<int32_t*>(smem + J.lds_stacks) + wave * J.lds_stack * 64 + lane;
       const SpillStack<STACK> stk{tstk, J.spill + static_cast<int64_t>(slot) * J.spill_depth * 64 + lane,
                                   J.lds_stack, J.lds_stack + J.spill_depth};
-      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, stk, w, rtab, otab);
+      render_stream<SpillStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, stk, w, rtab);
     } else {
       render_stream<LdsStack<STACK>, COUNT, WIDE, TEXF, kGeomTreelet, RING, PRIMS>(L, C, J, LdsStack<STACK>{lstk}, w,
-                                                                                rtab, otab);
+                                                                                rtab);
     }
     flush_stats<COUNT>(J, w, lane_now());
     trace_wave(J, t0, w.pixels, lane_now(), blockIdx.x * wpb + wave, (blockIdx.x << 8) | wave);
   } else {
     render_lds_scene<STACK, SPILL, COUNT, WAVES, WIDE, TEXF, RING, PRIMS>(S, C, J, smem, kFill, wpb, t0, lane, wave,
-                                                                          lstk, lstk16, rtab, otab);
+                                                                          lstk, lstk16, rtab);
   }
 }
 
@@ -1936,8 +1829,6 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   off = a16(off + int64_t(S.num_perlins) * 768 * 4);
   const int64_t ring = off;  // RING kernels (J->ring_log2 >= 0): per-wave batch tables
   if (J && J->ring_log2 >= 0) off += int64_t(waves) * kRingEntries * 4;
-  const int64_t pairs = off;  // sphere-only kernels: leaf_pairs' 64-byte owner table per wave
-  if (RTG_LEAF_PAIRS && S.ref_mode == 1) off = a16(off + int64_t(waves) * 64);
   if (off > 160 * 1024) return -1;
   if (J) {
     J->lds_materials = static_cast<int32_t>(materials);
@@ -1950,7 +1841,6 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
     J->lds_perlin_vec = static_cast<int32_t>(pvec);
     J->lds_perlin_perm = static_cast<int32_t>(pperm);
     J->lds_ring = static_cast<int32_t>(ring);
-    J->lds_pairs = static_cast<int32_t>(pairs);
   }
   return static_cast<int>(off);
 }
@@ -1960,18 +1850,15 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
 int lds_layout_treelet(DevScene* S, int stack, int waves, DevJob* J) {
   const int64_t stacks = int64_t(waves) * stack * 64 * 4;
   const int64_t ring = J->ring_log2 >= 0 ? int64_t(waves) * kRingEntries * 4 : 0;  // RING: batch tables
-  // sphere-only kernels: leaf_pairs' 64-byte owner table per wave
-  const int64_t pairs = RTG_LEAF_PAIRS && S->ref_mode == 1 && S->tex_full == 0 ? int64_t(waves) * 64 : 0;
-  const int64_t room = 160 * 1024 - stacks - ring - pairs;
+  const int64_t room = 160 * 1024 - stacks - ring;
   const int64_t nb = node_bytes(S->node_width);
   if (S->node_width < 4 || room < nb) return -1;
   const int64_t nodes = std::min<int64_t>(S->num_nodes, room / nb);
   S->treelet_bytes = static_cast<int32_t>(nodes * nb);
   J->lds_ring = static_cast<int32_t>(stacks);
-  J->lds_pairs = static_cast<int32_t>(stacks + ring);
-  J->lds_nodes = static_cast<int32_t>(stacks + ring + pairs);
+  J->lds_nodes = static_cast<int32_t>(stacks + ring);
   J->lds_stacks = 0;
-  return static_cast<int>(stacks + ring + pairs + nodes * nb);
+  return static_cast<int>(stacks + ring + nodes * nb);
 }
 
 // The dual launch (rtg_api.cpp) needs the 16-wave workgroup's four waves and the 4-wave workgroup's

@@ -1,6 +1,7 @@
 #!/bin/bash
 # GPU session (round 6): leaf_pairs A/B on configs 2, 5 and 3 (same box, alternating rounds), counts and
-# schedule diagnostics of both builds. Build first: make -C raytracing-practice_amd && tools/build_ab.sh nopairs -DRTG_LEAF_PAIRS=0
+# schedule diagnostics of both builds. The prototype left the product (measured rejection, profiles/r06_pairs):
+# git apply tools/experiments/leaf_pairs.patch, then make -C raytracing-practice_amd && tools/build_ab.sh nopairs -DRTG_LEAF_PAIRS=0
 set -u
 OUT=gpurun_out/${AB_OUT:-r06_pairs}
 mkdir -p $OUT

@@ -1210,6 +1210,42 @@ def test_render_plan_names_the_kernel(gpu_lib, scenes, name, grid, W, schedule, 
         assert p.partial_bytes == 2048 * 63 * 1024 + 8 * 2048 < H * W * 12 * 63 // 40
 
 
+def test_bench_rtg_gather_check_world_of_one(tmp_path):
+    """bench.py's N > 1 cross-check of the product gather (rtg_gather_check: rtg_comm_create_rank with the id
+    broadcast over torch.distributed, rtg_gather_rows once per timed step, each call timed, the library's
+    allocations counted) only runs on a multi-GPU node; here the same function at world 1 (gloo for the id
+    broadcast, a one-rank RCCL communicator): status ok, the frame byte-identical, 4 calls, no allocation
+    after the first."""
+    import json
+    import socket
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    script = f"""
+import json, os, sys
+sys.path.insert(0, {REPO!r})
+sys.path.insert(0, os.path.join({REPO!r}, "raytracing-practice_amd", "python"))
+import torch, torch.distributed as dist
+import rtgpu, bench
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{port}")
+dist.init_process_group("gloo", rank=0, world_size=1)
+lib = rtgpu.Library()
+H, W = 54, 96
+shard = torch.rand((H, W, 3), device="cuda")
+rec = bench.rtg_gather_check(lib, dist, torch, 1, 0, 0, H, W, shard, shard.clone(),
+                             torch.cuda.current_stream().cuda_stream, 4)
+print(json.dumps(rec))
+dist.destroy_process_group()
+"""
+    r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert rec["status"] == "ok" and rec["identical_to_timed_frame"] is True and rec["ranks_seen"] == 1
+    assert rec["calls"] == 4 and rec["allocations_after_first_call"] == 0 and rec["gather_ms"] > 0
+
+
 def test_bench_two_ranks_rehearsal(tmp_path):
     """bench.py's N > 1 flow (interleaved shards, the gather on rank 0, per-rank records, the per-pixel
     check of the gathered frame against cpu_ref32, max-over-ranks timing) with two ranks on this one GPU

@@ -831,9 +831,10 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         return false;
       }
     }
-    out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_x, pl.perm_x + 256);
-    out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_y, pl.perm_y + 256);
-    out->perlin_perm.insert(out->perlin_perm.end(), pl.perm_z, pl.perm_z + 256);
+    // entry i of each axis holds perm[i] | perm[(i + 1) & 255] << 8: a noise lookup reads both corner
+    // entries of an axis with one LDS instruction (3 per octave instead of 6)
+    for (const auto* perm : {pl.perm_x, pl.perm_y, pl.perm_z})
+      for (int i = 0; i < 256; ++i) out->perlin_perm.push_back(perm[i] | (perm[(i + 1) & 255] << 8));
   }
   phase("materials");
   return true;

@@ -751,9 +751,11 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
   const float ww = w * w * (3.0f - 2.0f * w);
   // the six permutation entries are fetched before any of them is used (round 2: one LDS round trip
   // instead of dependent ones per octave; config 3 shades 7 octaves per ground hit)
-  const int px[2] = {perm[i & 255], perm[(i + 1) & 255]};
-  const int py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
-  const int pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
+  // (an entry packs perm[i] and perm[(i + 1) & 255], rtg_api.cpp compile_scene)
+  const int ex = perm[i & 255], ey = perm[256 + (j & 255)], ez = perm[512 + (k & 255)];
+  const int px[2] = {ex & 255, ex >> 8};
+  const int py[2] = {ey & 255, ey >> 8};
+  const int pz[2] = {ez & 255, ez >> 8};
   float accum = 0.0f;
   // the corner gradients in pairs (di, dj fixed; dk = 0, 1), each pair fetched (xyz only) before it
   // is used and the sum in the reference's corner order: fetching all eight float4s at once (round 2)

@@ -610,6 +610,53 @@ def test_ground_and_one_sphere(gpu_lib, oracle, bvh):
         assert np.array_equal(g, g2) and st2.segments == st.segments
 
 
+def test_three_perlin_tables_match_oracle(gpu_lib, oracle):
+    """Three noise textures on three different perlin tables (perlin.hpp:95-158; the device packs each
+    axis's permutation pairs per table, rtg_api.cpp compile_scene), one of them under a checker: the LDS
+    schedule (tables in LDS) and the plain-grid schedule (tables through L1/L2) both give cpu_ref32's frame."""
+    import ctypes as C
+
+    rng = np.random.default_rng(20261018)
+    P = (rtgpu.rtg_perlin * 3)()
+    for pl in P:
+        v = rng.uniform(-1.0, 1.0, (256, 3))
+        v /= np.linalg.norm(v, axis=1, keepdims=True)
+        for i in range(256):
+            pl.randvec[i][0], pl.randvec[i][1], pl.randvec[i][2] = v[i]
+        for name in ("perm_x", "perm_y", "perm_z"):
+            getattr(pl, name)[:] = [int(x) for x in rng.permutation(256)]
+    texs = [rtgpu.rtg_texture(type=rtgpu.RTG_TEX_NOISE, perlin=k, scale=s)
+            for k, s in ((0, 4.0), (1, 2.5), (2, 7.0))]
+    texs.append(rtgpu.rtg_texture(type=rtgpu.RTG_TEX_SOLID, color=rtgpu.D3(0.9, 0.3, 0.2)))
+    texs.append(rtgpu.rtg_texture(type=rtgpu.RTG_TEX_CHECKER, even=3, odd=2, scale=0.8))
+    mats = [rtgpu.rtg_material(type=rtgpu.RTG_MAT_LAMBERTIAN, texture=t) for t in (0, 1, 4)]
+
+    def ball(c, r, m):
+        return rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_SPHERE, material=m, p0=rtgpu.D3(*c), p1=rtgpu.D3(*c),
+                                   radius=r)
+
+    prims = [ball((0, -1000, 0), 1000.0, 0), ball((-1.1, 1, 0), 1.0, 1), ball((1.1, 1, 0), 1.0, 2)]
+    d = _desc(prims, mats, texs)
+    d.perlins, d.num_perlins = C.cast(P, C.POINTER(rtgpu.rtg_perlin)), 3
+    d._keep = d._keep + (P,)
+    cam = rtgpu.camera(image_width=64, aspect_ratio=1.5, samples_per_pixel=4, max_depth=6,
+                       background=(0.7, 0.8, 1.0), lookfrom=(0, 2, 7), lookat=(0, 1, 0))
+    o, segs = oracle.render_f32(d, cam)
+    ds = gpu_lib.scene_create(d)
+    g, st = ds.render_host(cam)
+    assert_parity(g, o, st, segs)
+    H = gpu_lib.camera_resolve(cam).image_height
+    out = np.zeros((H, 64, 3), dtype=np.float32)
+    job = rtgpu.rtg_render_desc(rtgpu.DEFAULT_SEED, 0, 1, 0, rtgpu.RTG_RENDER_SCHEDULE(4), None)
+    st4 = rtgpu.rtg_render_stats()
+    gpu_lib.check("rtg_render", gpu_lib.lib.rtg_render(ds.handle, C.byref(cam), C.byref(job), out.ctypes.data,
+                                                       C.byref(st4)))
+    ds.close()
+    assert np.array_equal(out, g) and st4.segments == st.segments
+    # the three tables really differ on this frame: the balls' noise is not one texture
+    assert not np.array_equal(g[:, :32], g[:, 32:][:, ::-1])
+
+
 @pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])
 def test_exact_t_ties_match_oracle(gpu_lib, oracle, bvh):
     """The exact-t tie rule: three identical quads hit at bit-identical

@@ -831,10 +831,15 @@ bool compile_scene(const rtg_scene_desc* d, HostScene* out, std::string* err) {
         return false;
       }
     }
-    // entry i of each axis holds perm[i] | perm[(i + 1) & 255] << 8: a noise lookup reads both corner
-    // entries of an axis with one LDS instruction (3 per octave instead of 6)
-    for (const auto* perm : {pl.perm_x, pl.perm_y, pl.perm_z})
-      for (int i = 0; i < 256; ++i) out->perlin_perm.push_back(perm[i] | (perm[(i + 1) & 255] << 8));
+    // the packed words of rtg_internal.hpp (kPerlinPermWords): a noise octave reads both corner entries
+    // of every axis with three LDS instructions, and two XORs per word give two corners' gradient offsets
+    auto off = [](int32_t v) { return static_cast<uint32_t>(v) << 4; };
+    for (int i = 0; i < 256; ++i) out->perlin_perm.push_back(off(pl.perm_x[i]) | off(pl.perm_x[(i + 1) & 255]) << 16);
+    for (const int32_t* perm : {pl.perm_y, pl.perm_z})
+      for (int i = 0; i < 256; ++i) {
+        out->perlin_perm.push_back(off(perm[i]) * 0x10001u);
+        out->perlin_perm.push_back(off(perm[(i + 1) & 255]) * 0x10001u);
+      }
   }
   phase("materials");
   return true;
@@ -1145,7 +1150,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc_in, int32_t device, rtg_s
   s->dev.images = reinterpret_cast<const int4*>(base + parts[6].off);
   s->dev.texels = reinterpret_cast<const uint8_t*>(base + parts[7].off);
   s->dev.perlin_vec = reinterpret_cast<const float4*>(base + parts[8].off);
-  s->dev.perlin_perm = reinterpret_cast<const int32_t*>(base + perm_off);
+  s->dev.perlin_perm = reinterpret_cast<const uint32_t*>(base + perm_off);
   s->dev.tie_rank = reinterpret_cast<const int32_t*>(base + rank_off);
   s->dev.num_nodes = hs.num_nodes;
   s->dev.root_code = 0;
@@ -1178,7 +1183,7 @@ rtg_status rtg_scene_create(const rtg_scene_desc* desc_in, int32_t device, rtg_s
   for (int32_t m = 0; m < desc->num_materials; ++m)
     if (desc->materials[m].type == RTG_MAT_METAL || desc->materials[m].type == RTG_MAT_DIELECTRIC)
       s->dev.diffuse_only = 0;
-  s->dev.num_perlins = static_cast<int32_t>(hs.perlin_perm.size() / 768);
+  s->dev.num_perlins = static_cast<int32_t>(hs.perlin_perm.size() / kPerlinPermWords);
   s->num_cus = prop.multiProcessorCount;
   // trees too large for any LDS schedule render on the treelet schedule: keep their node array on the
   // host for the hot-treelet renumbering (device-built trees are downloaded once, on the first tuning)
@@ -1259,8 +1264,8 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
   if (c[24] != 0)
     return fail(RTG_E_HIP, "tile-ring slot waits timed out (frame incomplete) in " + std::to_string(c[24]) + " waves");
   if (c[7] != 0)
-    return fail(RTG_E_UNSUPPORTED, "the 16-bit LDS stack layout cannot hold this tree's codes in " +
-                                       std::to_string(c[7]) + " workgroups (nothing rendered)");
+    return fail(RTG_E_UNSUPPORTED, "the LDS layout (16-bit stack codes, or perlin rows below 64 KiB) does not "
+                                   "hold in " + std::to_string(c[7]) + " workgroups (nothing rendered)");
   return RTG_OK;
 }
 

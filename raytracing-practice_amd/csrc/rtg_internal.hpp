@@ -9,7 +9,7 @@
 //   materials: float4[2*num_mats]    {type, texture, fuzz, eta}, {albedo.xyz, -}
 //   textures : float4[2*num_tex]     {type, even, odd, scale}, {color.xyz, image|perlin}
 //   images   : int4[num_images]      {width, height, byte offset lo, byte offset hi} + uint8 texels
-//   perlin   : per table float4 randvec[256] then int32 perm[3][256]
+//   perlin   : per table float4 randvec[256]; permutation words (kPerlinPermWords per table, below)
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -23,6 +23,12 @@ namespace rtg {
 
 constexpr int32_t kEmptyChild = INT32_MIN;  // child slot with an inverted box; never visited
 constexpr int32_t kQuadRefBit = 1 << 30;
+// A perlin table's permutations as the noise lookup reads them (perlin.hpp:95-158): 16-bit lanes, each a
+// gradient index times 16 (its byte offset among the 16-B gradient rows); X[i] = (p_x[i], p_x[i+1]) in one
+// word, Y[j] = {(p_y[j], p_y[j]), (p_y[j+1], p_y[j+1])} and Z[k] = {(p_z[k], p_z[k]), (p_z[k+1], p_z[k+1])}
+// in two (indices + 1 mod 256), so X[i] ^ Y[j][dj] ^ Z[k][dk] holds the offsets of corners (0, dj, dk) and
+// (1, dj, dk). Words: X 256, then Y 2 x 256, then Z 2 x 256
+constexpr int32_t kPerlinPermWords = 1280;
 
 // A float view of the scene, ready for upload. Produced on the host from rtg_scene_desc.
 struct HostScene {
@@ -35,7 +41,7 @@ struct HostScene {
   std::vector<int32_t> image_hdr;  // 4 ints per image
   std::vector<uint8_t> texels;
   std::vector<float> perlin_vec;   // 4 floats * 256 per table
-  std::vector<int32_t> perlin_perm;  // 3*256 per table
+  std::vector<uint32_t> perlin_perm;  // kPerlinPermWords per table
   // exact-t tie rule: the input (list-order) index of every sphere slot, then of every
   // quad slot; read by the kernels only when a primitive's root equals the closest hit so far
   std::vector<int32_t> tie_rank;
@@ -161,7 +167,7 @@ struct DevScene {
   const int4* images;
   const uint8_t* texels;
   const float4* perlin_vec;
-  const int32_t* perlin_perm;
+  const uint32_t* perlin_perm;
   int64_t num_nodes;
   int64_t num_refs;
   int64_t num_spheres;
@@ -174,7 +180,7 @@ struct DevScene {
   int32_t ref_mode;
   int32_t tex_full;  // 1 when some texture is an image or noise texture (kernel variant selector)
   int32_t diffuse_only;  // 1 when no material is metal or dielectric (kernel variant selector)
-  int32_t num_perlins;  // perlin tables (256 gradients + 3 x 256 permutations each)
+  int32_t num_perlins;  // perlin tables (256 gradients + kPerlinPermWords permutation words each)
   // 4-wide trees: inner-node codes are byte offsets from `nodes`, the root's is root_code (0 in
   // HBM; the persistent kernel rebases its LDS copy so codes are absolute LDS addresses) and every
   // valid one is below node_limit (root_code + num_nodes * 112)

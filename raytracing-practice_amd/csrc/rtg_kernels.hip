@@ -742,20 +742,32 @@ __device__ __forceinline__ void leaf_step(Trav& t, const DevScene& S, V3 o, V3 d
 
 // ---------------------------------------------------------------------------------------
 // Textures (texture.hpp:34-151, perlin.hpp:95-158, 219-255)
-__device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
+// LDS: the gradient rows and permutation words are the workgroup's LDS copy, whose Z words carry the
+// rows' LDS address (render_lds_scene), so a corner's offset is its row's LDS address; else offsets are
+// relative to `vec` (global memory)
+template <bool LDS>
+__device__ float perlin_noise(const float4* vec, const uint32_t* perm, V3 p) {
   const float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
   const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
   const int i = static_cast<int>(fx), j = static_cast<int>(fy), k = static_cast<int>(fz);
   const float uu = u * u * (3.0f - 2.0f * u);
   const float vv = v * v * (3.0f - 2.0f * v);
   const float ww = w * w * (3.0f - 2.0f * w);
-  // the six permutation entries are fetched before any of them is used (round 2: one LDS round trip
-  // instead of dependent ones per octave; config 3 shades 7 octaves per ground hit)
-  // (an entry packs perm[i] and perm[(i + 1) & 255], rtg_api.cpp compile_scene)
-  const int ex = perm[i & 255], ey = perm[256 + (j & 255)], ez = perm[512 + (k & 255)];
-  const int px[2] = {ex & 255, ex >> 8};
-  const int py[2] = {ey & 255, ey >> 8};
-  const int pz[2] = {ez & 255, ez >> 8};
+  // both corner entries of each axis in one read (the words of rtg_internal.hpp kPerlinPermWords), all
+  // three issued before any is used (round 2: one LDS round trip per octave; config 3 shades 7 octaves
+  // per ground hit); X ^ Y[dj] ^ Z[dk] holds the gradient offsets of corners (0, dj, dk) and (1, dj, dk)
+  const uint32_t px = perm[i & 255];
+  const uint2 py = reinterpret_cast<const uint2*>(perm + 256)[j & 255];
+  const uint2 pz = reinterpret_cast<const uint2*>(perm + 768)[k & 255];
+  auto grad = [&](uint32_t off) -> V3 {
+    if constexpr (LDS) {
+      typedef float nf3 __attribute__((ext_vector_type(3)));
+      const nf3 g = *reinterpret_cast<__attribute__((address_space(3))) const nf3*>(static_cast<uintptr_t>(off));
+      return v3(g.x, g.y, g.z);
+    } else {
+      return xyz(*reinterpret_cast<const float4*>(reinterpret_cast<const unsigned char*>(vec) + off));
+    }
+  };
   float accum = 0.0f;
   // the corner gradients in pairs (di, dj fixed; dk = 0, 1), each pair fetched (xyz only) before it
   // is used and the sum in the reference's corner order: fetching all eight float4s at once (round 2)
@@ -765,8 +777,10 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
   for (int di = 0; di < 2; ++di) {
 #pragma unroll
     for (int dj = 0; dj < 2; ++dj) {
-      const int pij = px[di] ^ py[dj];
-      const V3 g0 = xyz(vec[pij ^ pz[0]]), g1 = xyz(vec[pij ^ pz[1]]);
+      const uint32_t pxy = px ^ (dj ? py.y : py.x);
+      const uint32_t o0 = di ? (pxy ^ pz.x) >> 16 : (pxy ^ pz.x) & 0xffffu;
+      const uint32_t o1 = di ? (pxy ^ pz.y) >> 16 : (pxy ^ pz.y) & 0xffffu;
+      const V3 g0 = grad(o0), g1 = grad(o1);
 #pragma unroll
       for (int dk = 0; dk < 2; ++dk) {
         const V3 c = dk ? g1 : g0;
@@ -776,16 +790,20 @@ __device__ float perlin_noise(const float4* vec, const int32_t* perm, V3 p) {
         const float fw = dk ? ww : (1.0f - ww);
         accum = fmaf(fu * fv * fw, dot(c, wv), accum);
       }
+      // one pair of gradient rows in flight at a time: the scheduler otherwise issues six of the eight
+      // reads at once and the textured kernel spills 16 B/lane (round 6)
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   return accum;
 }
 
-__device__ float perlin_turb(const float4* vec, const int32_t* perm, V3 p) {
+template <bool LDS>
+__device__ float perlin_turb(const float4* vec, const uint32_t* perm, V3 p) {
   float accum = 0.0f, weight = 1.0f;
   V3 tp = p;
   for (int i = 0; i < 7; ++i) {  // not unrolled: 2 octaves at once ±0, all 7 spill 576 B/lane (7x slower)
-    accum = fmaf(weight, perlin_noise(vec, perm, tp), accum);
+    accum = fmaf(weight, perlin_noise<LDS>(vec, perm, tp), accum);
     weight *= 0.5f;
     tp = scl(2.0f, tp);
   }
@@ -794,7 +812,8 @@ __device__ float perlin_turb(const float4* vec, const int32_t* perm, V3 p) {
 
 // FULL = false compiles solid and checker textures only (scenes without image / noise textures):
 // the perlin and image paths cost ~12 vector registers the common scenes would otherwise spill.
-template <bool FULL>
+// LDS_TAB: the perlin tables are the workgroup's LDS copy (perlin_noise)
+template <bool FULL, bool LDS_TAB = false>
 __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3 p) {
   // a checker resolves to another texture: one trip per nesting level (solid under checker: 2);
   // not unrolled (16 unrolled copies cost ~70 scalar branch instructions per shade)
@@ -837,8 +856,8 @@ __device__ V3 texture_value(const DevScene& S, int32_t tex, float u, float v, V3
     if (FULL && type == RTG_TEX_NOISE) {
       const int pt = ibits(t1.w);
       const float4* vec = S.perlin_vec + pt * 256;
-      const int32_t* perm = S.perlin_perm + pt * 768;
-      const float t = perlin_turb(vec, perm, p);
+      const uint32_t* perm = S.perlin_perm + pt * kPerlinPermWords;
+      const float t = perlin_turb<LDS_TAB>(vec, perm, p);
       const float s = 0.5f * (1.0f + sin_spec(fmaf(t0.w, p.z, 10.0f * t)));
       return v3(s, s, s);
     }
@@ -893,7 +912,8 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
 // (the cache-read schedules: two independent loads instead of a dependent pair)
 // PRIMS: the scene class (kPrimsAny ...): sphere-only kernels shade spheres only, quad-only ones quads
 // only (chosen only without a sphere occluder), diffuse-only ones have no metal / dielectric code
-template <bool FULL, bool MAT = false, int PRIMS = kPrimsAny>
+// LDS_TAB: the perlin tables are in LDS (the whole-scene LDS schedule's textured kernels)
+template <bool FULL, bool MAT = false, int PRIMS = kPrimsAny, bool LDS_TAB = false>
 __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, int32_t mat_hit = 0) {
   V3 p, outward;
   float u = 0.0f, v = 0.0f;
@@ -936,7 +956,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
 
   if (type == RTG_MAT_DIFFUSE_LIGHT) {
     if (needs_uv) sphere_uv();
-    const V3 e = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);  // < 0: solid colour inline
+    const V3 e = tex < 0 ? xyz(m1) : texture_value<FULL, LDS_TAB>(S, tex, u, v, p);  // < 0: solid colour inline
     ps.L = vfma(ps.T, e, ps.L);
     return false;
   }
@@ -947,7 +967,7 @@ __device__ bool shade(const DevScene& S, PathState& ps, int32_t ref, float t, in
     // stayed live across the texture evaluation and went to scratch in the textured kernel (round 6)
     if (kDiffuse || type == RTG_MAT_LAMBERTIAN) {
       if (needs_uv) sphere_uv();
-      att = tex < 0 ? xyz(m1) : texture_value<FULL>(S, tex, u, v, p);
+      att = tex < 0 ? xyz(m1) : texture_value<FULL, LDS_TAB>(S, tex, u, v, p);
     }
     // both scatter around a random unit vector: one sampling code path for the lanes of either
     const V3 r = random_unit_vector(ps.rng);
@@ -1435,7 +1455,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
         alive_path = false;
       } else {
         if (COUNT) ++w.hits;
-        alive_path = shade<TEXF, GEOM != kGeomLds, PRIMS>(S, ps, tr.best, tr.tbest, tr.mat);
+        alive_path = shade<TEXF, GEOM != kGeomLds, PRIMS, GEOM == kGeomLds>(S, ps, tr.best, tr.tbest, tr.mat);
         if (alive_path && --ps.depth <= 0) alive_path = false;
       }
       uint64_t t_end = 0;
@@ -1541,10 +1561,23 @@ __device__ __forceinline__ void render_lds_scene(const DevScene& S, const DevCam
   if (S.ref_mode == 0)
     for (int64_t k = threadIdx.x; k < S.num_refs; k += kFill) l_refs[k] = S.refs[k];
   float4* l_pvec = reinterpret_cast<float4*>(smem + J.lds_perlin_vec);
-  int32_t* l_pperm = reinterpret_cast<int32_t*>(smem + J.lds_perlin_perm);
+  uint32_t* l_pperm = reinterpret_cast<uint32_t*>(smem + J.lds_perlin_perm);
   if (TEXF) {
+    // the Z words of table t carry the LDS address of its gradient rows in both 16-bit lanes (the host
+    // plans them from LDS address 0: 4096-aligned, below 64 KiB, so an OR of disjoint bits); if the
+    // dynamic-LDS base ever moves them elsewhere, report and render nothing
+    const uint32_t vbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                               (__attribute__((address_space(3))) unsigned char*)smem)) + J.lds_perlin_vec;
+    if ((vbase & 4095u) != 0 || vbase + static_cast<uint32_t>(S.num_perlins) * 4096u > 65536u) {
+      if (threadIdx.x == 0) atomicAdd(&J.counters[7], 1ull);
+      return;
+    }
     for (int k = threadIdx.x; k < S.num_perlins * 256; k += kFill) l_pvec[k] = S.perlin_vec[k];
-    for (int k = threadIdx.x; k < S.num_perlins * 768; k += kFill) l_pperm[k] = S.perlin_perm[k];
+    for (int k = threadIdx.x; k < S.num_perlins * kPerlinPermWords; k += kFill) {
+      const int t = k / kPerlinPermWords;
+      const uint32_t b = vbase + static_cast<uint32_t>(t) * 4096u;
+      l_pperm[k] = S.perlin_perm[k] ^ (k - t * kPerlinPermWords >= 768 ? b * 0x10001u : 0u);
+    }
   }
   __syncthreads();
   DevScene L = S;
@@ -1810,9 +1843,15 @@ KernelResources kernel_resources(const void* fn) {
 int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   auto a16 = [](int64_t x) { return (x + 15) & ~int64_t(15); };
   // the node array first (at LDS address 0: inner-node codes are its byte offsets, <= 15 bits for
-  // trees of <= 292 4-wide nodes, LdsStack16), then the traversal stacks (esz bytes per entry)
-  const int64_t nodes = 0;
-  int64_t off = a16(S.num_nodes * (S.node_width == 4 ? 112 : 64));
+  // trees of <= 292 4-wide nodes, LdsStack16), then the traversal stacks (esz bytes per entry). Scenes
+  // with noise textures (32-bit stacks) put the perlin gradient rows first instead: the noise lookup's
+  // offsets carry the table's LDS address in 16 bits (perlin_noise), so at most 16 tables. Kernels
+  // without image / noise textures (tex_full 0) copy no tables
+  const int64_t perlins = S.tex_full ? S.num_perlins : 0;
+  if (perlins > 16) return -1;
+  const int64_t pvec = 0;
+  const int64_t nodes = perlins * 256 * 16;
+  int64_t off = a16(nodes + S.num_nodes * (S.node_width == 4 ? 112 : 64));
   const int64_t stacks = off;
   off = a16(off + int64_t(waves) * stack * 64 * esz);
   const int64_t spheres = off;
@@ -1825,10 +1864,8 @@ int lds_layout(const DevScene& S, int stack, int waves, int esz, DevJob* J) {
   off = a16(off + int64_t(S.num_materials) * 32);
   const int64_t textures = off;
   off = a16(off + int64_t(S.num_textures) * 32);
-  const int64_t pvec = off;
-  off = a16(off + int64_t(S.num_perlins) * 256 * 16);
   const int64_t pperm = off;
-  off = a16(off + int64_t(S.num_perlins) * 768 * 4);
+  off = a16(off + perlins * kPerlinPermWords * 4);
   const int64_t ring = off;  // RING kernels (J->ring_log2 >= 0): per-wave batch tables
   if (J && J->ring_log2 >= 0) off += int64_t(waves) * kRingEntries * 4;
   if (off > 160 * 1024) return -1;

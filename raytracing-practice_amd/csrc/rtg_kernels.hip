@@ -750,9 +750,11 @@ __device__ float perlin_noise(const float4* vec, const uint32_t* perm, V3 p) {
   const float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
   const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
   const int i = static_cast<int>(fx), j = static_cast<int>(fy), k = static_cast<int>(fz);
-  const float uu = u * u * (3.0f - 2.0f * u);
-  const float vv = v * v * (3.0f - 2.0f * v);
-  const float ww = w * w * (3.0f - 2.0f * w);
+  // Hermite weights u u (3 - 2 u) (perlin.hpp:226-228): 2 u is exact, so the one-rounding fmaf(-2, u, 3)
+  // is bit for bit the spec's 3 - 2 u (cpu_ref32), one VALU op fewer per axis
+  const float uu = u * u * fmaf(-2.0f, u, 3.0f);
+  const float vv = v * v * fmaf(-2.0f, v, 3.0f);
+  const float ww = w * w * fmaf(-2.0f, w, 3.0f);
   // both corner entries of each axis in one read (the words of rtg_internal.hpp kPerlinPermWords), all
   // three issued before any is used (round 2: one LDS round trip per octave; config 3 shades 7 octaves
   // per ground hit); X ^ Y[dj] ^ Z[dk] holds the gradient offsets of corners (0, dj, dk) and (1, dj, dk)
@@ -778,8 +780,9 @@ __device__ float perlin_noise(const float4* vec, const uint32_t* perm, V3 p) {
 #pragma unroll
     for (int dj = 0; dj < 2; ++dj) {
       const uint32_t pxy = px ^ (dj ? py.y : py.x);
-      const uint32_t o0 = di ? (pxy ^ pz.x) >> 16 : (pxy ^ pz.x) & 0xffffu;
-      const uint32_t o1 = di ? (pxy ^ pz.y) >> 16 : (pxy ^ pz.y) & 0xffffu;
+      const uint32_t ph = di ? pxy >> 16 : pxy;
+      const uint32_t o0 = (ph ^ pz.x) & 0xffffu;
+      const uint32_t o1 = (ph ^ pz.y) & 0xffffu;
       const V3 g0 = grad(o0), g1 = grad(o1);
 #pragma unroll
       for (int dk = 0; dk < 2; ++dk) {

@@ -96,20 +96,26 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 31;
   return z;
 }
-__device__ __forceinline__ float uniform(uint64_t& s) {  // random_double(), [0,1), 24 bits
+// One draw's 24 bits as an exact float integer in [0, 2^24): uniform() = draw24() * 2^-24. Callers that
+// scale U by a power of two or add a constant fold the scaling into one exact product (and the constant
+// into an fmaf, whose one rounding is the spec's rounding of the sum): bit-identical, fewer VALU ops.
+__device__ __forceinline__ float draw24(uint64_t& s) {
   s = s * 6364136223846793005ull + 1442695040888963407ull;
   // bits 63..40, converted by an explicit v_cvt_f32_u32: the compiler widens a plain
   // (float)(uint32_t)(s >> 40) back into a 64-bit integer-to-float expansion (+6 VALU per draw)
   const uint32_t top = static_cast<uint32_t>(s >> 32) >> 8;
   float f;
   asm("v_cvt_f32_u32 %0, %1" : "=v"(f) : "v"(top));
-  return f * 5.9604644775390625e-8f;
+  return f;
+}
+__device__ __forceinline__ float uniform(uint64_t& s) {  // random_double(), [0,1), 24 bits
+  return draw24(s) * 5.9604644775390625e-8f;
 }
 
 // sin and cos of 2*pi*u, u in [0,1): quadrant reduction and Taylor polynomials on [-pi/4, pi/4),
-// plain fp32 multiply / fmaf only, so oracle/cpu_ref.c (sincos_turn) reproduces every bit.
-__device__ __forceinline__ void sincos_turn(float u, float& sn, float& cs) {
-  const float t = 4.0f * u;
+// plain fp32 multiply / fmaf only, so oracle/cpu_ref.c (sincos_turn) reproduces every bit. Takes
+// t = 4u (for a draw: draw24 * 2^-22, the spec's 4 * (draw24 * 2^-24) exactly)
+__device__ __forceinline__ void sincos_turn4(float t, float& sn, float& cs) {
   const float q = floorf(t);
   const float x = (t - q - 0.5f) * 1.57079637f;
   const float x2 = x * x;
@@ -176,10 +182,10 @@ __device__ __forceinline__ float acos_spec(float v) {
 // the azimuth from a second U. The reference's rejection loop would make every wave wait for its
 // unluckiest lane (~5 tries for 30 lanes at acceptance pi/6); this costs two draws, always.
 __device__ __forceinline__ V3 random_unit_vector(uint64_t& s) {
-  const float z = 1.0f - 2.0f * uniform(s);
+  const float z = fmaf(-0x1p-23f, draw24(s), 1.0f);  // 1 - 2U: 2U = draw24 * 2^-23 exactly
   const float r = sqrt_rn(fmaxf(0.0f, fmaf(-z, z, 1.0f)));
   float sn, cs;
-  sincos_turn(uniform(s), sn, cs);
+  sincos_turn4(draw24(s) * 0x1p-22f, sn, cs);
   return v3(r * cs, r * sn, z);
 }
 
@@ -883,8 +889,8 @@ struct PathState {
 __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, uint64_t seed_mix,
                                              uint32_t pixel_id, uint32_t sample, int i, int j) {
   ps.rng = mix64(((static_cast<uint64_t>(pixel_id) << 32) | sample) ^ seed_mix);
-  const float ox = uniform(ps.rng) - 0.5f;
-  const float oy = uniform(ps.rng) - 0.5f;
+  const float ox = fmaf(draw24(ps.rng), 0x1p-24f, -0.5f);  // U - 0.5 (U exact: one rounding either way)
+  const float oy = fmaf(draw24(ps.rng), 0x1p-24f, -0.5f);
   const float fi = static_cast<float>(i) + ox;
   const float fj = static_cast<float>(j) + oy;
   const V3 p00 = v3(C.pixel00[0], C.pixel00[1], C.pixel00[2]);
@@ -896,7 +902,7 @@ __device__ __forceinline__ void start_sample(PathState& ps, const DevCamera& C, 
     // random_in_unit_disk (vec3.hpp:158-169), direct: radius sqrt(U), angle from a second U
     const float r = sqrt_rn(uniform(ps.rng));
     float sn, cs;
-    sincos_turn(uniform(ps.rng), sn, cs);
+    sincos_turn4(draw24(ps.rng) * 0x1p-22f, sn, cs);
     const float px = r * cs, py = r * sn;
     origin = madd(py, v3(C.defv[0], C.defv[1], C.defv[2]), madd(px, v3(C.defu[0], C.defu[1], C.defu[2]), origin));
   }

@@ -221,7 +221,8 @@ __device__ __forceinline__ float sphere_t(float4 s0, float4 s1, V3 o, V3 d, floa
     const double oy = static_cast<double>(o.y) - static_cast<double>(C.y);
     const double oz = static_cast<double>(o.z) - static_cast<double>(C.z);
     const double r = static_cast<double>(s0.w);
-    c = static_cast<float>((ox * ox + oy * oy + oz * oz) - r * r);
+    // r * r of a float r is exact in f64, so the fma's one rounding is the subtraction's
+    c = static_cast<float>(fma(-r, r, ox * ox + oy * oy + oz * oz));
     disc = fmaf(hb, hb, -(a * c));
   }
   if (disc < 0.0f) return -1.0f;
@@ -261,8 +262,10 @@ __device__ __forceinline__ float quad_t(const float4* q, V3 o, V3 d, float tmin,
   const V3 n = xyz(q4);
   const float denom = dot(n, d);
   if (fabsf(denom) < 1e-8f) return -1.0f;
-  const double dn = static_cast<double>(n.x) * o.x + static_cast<double>(n.y) * o.y +
-                    static_cast<double>(n.z) * o.z;
+  // products of two floats are exact in f64, so the fma chain rounds exactly where mul + add would
+  const double dn = fma(static_cast<double>(n.z), static_cast<double>(o.z),
+                        fma(static_cast<double>(n.y), static_cast<double>(o.y),
+                            static_cast<double>(n.x) * static_cast<double>(o.x)));
   const float num = static_cast<float>(static_cast<double>(q0.w) - dn);
   const float t = div_rn(num, denom);
   if (!(tmin <= t && t <= tmax)) return -1.0f;

@@ -610,14 +610,17 @@ def test_ground_and_one_sphere(gpu_lib, oracle, bvh):
         assert np.array_equal(g, g2) and st2.segments == st.segments
 
 
-def test_three_perlin_tables_match_oracle(gpu_lib, oracle):
-    """Three noise textures on three different perlin tables (perlin.hpp:95-158; the device packs each
-    axis's permutation pairs per table, rtg_api.cpp compile_scene), one of them under a checker: the LDS
-    schedule (tables in LDS) and the plain-grid schedule (tables through L1/L2) both give cpu_ref32's frame."""
+@pytest.mark.parametrize("tables,schedule", [(3, 3), (17, 5)])
+def test_perlin_tables_match_oracle(gpu_lib, oracle, tables, schedule):
+    """Noise textures on several perlin tables (perlin.hpp:95-158; the device's packed permutation words,
+    rtg_internal.hpp kPerlinPermWords), one of them under a checker. Up to 16 tables ride in LDS (their
+    rows' LDS addresses fit the 16-bit offsets): the default LDS schedule; 17 do not, so the plan falls to
+    the cache-read schedule with the tables in global memory. Both, and the plain grid, give cpu_ref32's
+    frame."""
     import ctypes as C
 
     rng = np.random.default_rng(20261018)
-    P = (rtgpu.rtg_perlin * 3)()
+    P = (rtgpu.rtg_perlin * tables)()
     for pl in P:
         v = rng.uniform(-1.0, 1.0, (256, 3))
         v /= np.linalg.norm(v, axis=1, keepdims=True)
@@ -625,24 +628,30 @@ def test_three_perlin_tables_match_oracle(gpu_lib, oracle):
             pl.randvec[i][0], pl.randvec[i][1], pl.randvec[i][2] = v[i]
         for name in ("perm_x", "perm_y", "perm_z"):
             getattr(pl, name)[:] = [int(x) for x in rng.permutation(256)]
-    texs = [rtgpu.rtg_texture(type=rtgpu.RTG_TEX_NOISE, perlin=k, scale=s)
-            for k, s in ((0, 4.0), (1, 2.5), (2, 7.0))]
+    scales = (4.0, 2.5, 7.0)
+    texs = [rtgpu.rtg_texture(type=rtgpu.RTG_TEX_NOISE, perlin=k, scale=scales[k % 3]) for k in range(tables)]
     texs.append(rtgpu.rtg_texture(type=rtgpu.RTG_TEX_SOLID, color=rtgpu.D3(0.9, 0.3, 0.2)))
-    texs.append(rtgpu.rtg_texture(type=rtgpu.RTG_TEX_CHECKER, even=3, odd=2, scale=0.8))
-    mats = [rtgpu.rtg_material(type=rtgpu.RTG_MAT_LAMBERTIAN, texture=t) for t in (0, 1, 4)]
+    texs.append(rtgpu.rtg_texture(type=rtgpu.RTG_TEX_CHECKER, even=tables, odd=tables - 1, scale=0.8))
+    # the ground, a checker ball over the last table, and a ball on every other table
+    mats = [rtgpu.rtg_material(type=rtgpu.RTG_MAT_LAMBERTIAN, texture=t) for t in range(tables - 1)]
+    mats.append(rtgpu.rtg_material(type=rtgpu.RTG_MAT_LAMBERTIAN, texture=tables + 1))
 
     def ball(c, r, m):
         return rtgpu.rtg_primitive(kind=rtgpu.RTG_PRIM_SPHERE, material=m, p0=rtgpu.D3(*c), p1=rtgpu.D3(*c),
                                    radius=r)
 
-    prims = [ball((0, -1000, 0), 1000.0, 0), ball((-1.1, 1, 0), 1.0, 1), ball((1.1, 1, 0), 1.0, 2)]
+    prims = [ball((0, -1000, 0), 1000.0, 0)]
+    for m in range(1, tables):
+        a = 2 * np.pi * m / tables
+        prims.append(ball((2.2 * np.cos(a), 0.8, 2.2 * np.sin(a)), 0.6, m))
     d = _desc(prims, mats, texs)
-    d.perlins, d.num_perlins = C.cast(P, C.POINTER(rtgpu.rtg_perlin)), 3
+    d.perlins, d.num_perlins = C.cast(P, C.POINTER(rtgpu.rtg_perlin)), tables
     d._keep = d._keep + (P,)
     cam = rtgpu.camera(image_width=64, aspect_ratio=1.5, samples_per_pixel=4, max_depth=6,
-                       background=(0.7, 0.8, 1.0), lookfrom=(0, 2, 7), lookat=(0, 1, 0))
+                       background=(0.7, 0.8, 1.0), lookfrom=(0, 3, 7), lookat=(0, 0.8, 0))
     o, segs = oracle.render_f32(d, cam)
     ds = gpu_lib.scene_create(d)
+    assert ds.plan(cam).schedule == schedule
     g, st = ds.render_host(cam)
     assert_parity(g, o, st, segs)
     H = gpu_lib.camera_resolve(cam).image_height
@@ -653,8 +662,8 @@ def test_three_perlin_tables_match_oracle(gpu_lib, oracle):
                                                        C.byref(st4)))
     ds.close()
     assert np.array_equal(out, g) and st4.segments == st.segments
-    # the three tables really differ on this frame: the balls' noise is not one texture
-    assert not np.array_equal(g[:, :32], g[:, 32:][:, ::-1])
+    # the tables really differ on this frame: no two balls show the same noise
+    assert len({g[r, c].tobytes() for r in range(H) for c in range(64)}) > 500
 
 
 @pytest.mark.parametrize("bvh", [rtgpu.RTG_BVH_SAH, rtgpu.RTG_BVH_GPU, rtgpu.RTG_BVH_MEDIAN])

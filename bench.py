@@ -426,7 +426,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    segs, kernel_ms = 0, []
+    segs, kernel_ms, st = 0, [], None
     # one event pair per timed step around the gather, on the render stream (torch's current stream)
     gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)] if world > 1 else [None] * args.steps
@@ -537,6 +537,10 @@ def main():
             "rays_per_sample": round(total_segs / samples, 4),
             "setup_ms": round((t_scene + t_create + t_prepare) * 1e3, 1),
             "setup": setup_ms,
+            # rtg_scene_prepare's cost-ordered tile hand-out (DESIGN.md §3 "tile order"): whether the timed
+            # frames used it (rank 0's last step) and its probe's host + device time within setup.prepare_ms
+            "tile_order": ({"used": bool(st.tile_order), "tune_ms": round(st.tile_order_tune_us / 1e3, 2)}
+                           if st is not None else None),
             "scene_build_ms": round(t_scene * 1e3, 1),
             "bvh": {"nodes": info.num_nodes, "depth": info.bvh_depth, "build_ms": round(info.build_ms, 1),
                     "upload_ms": round(info.upload_ms, 1)},

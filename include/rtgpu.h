@@ -231,7 +231,12 @@ typedef struct rtg_render_stats {
   /* ABI 6: RTG_RENDER_COUNT only: traversal-stack pushes that went to the global spill area (entries past
    * the stack's LDS part; deep trees such as config 5's), each a 4-B store and, at the pop, a 4-B load */
   uint64_t stack_spills;
-  uint64_t reserved_[3];
+  /* round 6, layout-compatible (the first of ABI 6's reserved words): 1 when this render handed its tiles out in
+   * the cost order rtg_scene_prepare tuned for its camera and shard (0: tile-major), and the host + probe time
+   * of the scene's last tile-order tuning in microseconds */
+  uint32_t tile_order;
+  uint32_t tile_order_tune_us;
+  uint64_t reserved_[2];
 } rtg_render_stats;
 
 typedef struct rtg_scene rtg_scene; /* opaque; owns the device copy of the scene */
@@ -324,7 +329,15 @@ typedef struct rtg_launch_plan {
 rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job,
                            rtg_launch_plan* out);
 
-/* Optional setup before the first render of a camera (and shard rows) on a scene (ABI 5 addition).
+/* Optional setup before the first render of a camera (and shard rows) on a scene (ABI 5 addition; the tile
+ * order since round 6, layout-compatible).
+ * Tile order (every default schedule, RTG_TILE_ORDER=1 default): a probe render of the camera and shard
+ * (counting kernel, up to 4 samples per pixel, one counter per 64-pixel tile) measures each tile's traced
+ * segments, and later renders of that camera and shard hand their tiles out most expensive first, so a
+ * launch ends on cheap units instead of one late expensive tile (an 8-GPU shard's tail). Frames and
+ * segment counts are unchanged: only which wave renders a unit, and when, changes. rtg_render_stats.tile_order
+ * says whether a render used it; renders of other cameras or shards (and the tile-ring kernels) keep the
+ * tile-major order.
  * Scenes whose BVH does not fit LDS render with the treelet schedule, which keeps a prefix of the
  * 4-wide node array in each workgroup's LDS; here a probe render (1 sample per pixel on about 2^19
  * pixels, every k-th row of the shard; counting kernel) counts every node's visits for this camera and the node array

@@ -329,6 +329,7 @@ Knobs read_knobs() {
   if (num("RTG_TILE_SLOTS", 0, 65536, &ts) && (ts & (ts - 1)) == 0) k.tile_slots = ts;
   num("RTG_TREELET_STACK", 4, 16, &k.treelet_stack);
   num("RTG_TREELET_HOT", 0, 1, &k.treelet_hot);
+  num("RTG_TILE_ORDER", 0, 1, &k.tile_order);
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -922,10 +923,18 @@ struct rtg_scene {
   // M of the culling margin the device node boxes are padded for (HostScene::origin_bound); raised,
   // with the boxes, when a camera lies farther out (ensure_origin_bound)
   double origin_bound = 0.0;
+  // cost-ordered tile hand-out (tune_tile_order): the tile handed out at each position for the camera and
+  // shard of order_key (order_tiles entries, device; grow-only), the probe's most expensive tile first
+  uint64_t order_key = 0;
+  int32_t* order_dev = nullptr;
+  int64_t order_tiles = 0, order_cap = 0;
+  double order_tune_ms = 0.0;
+  uint32_t* probe_tile_cost = nullptr;  // set only while the tile-cost probe runs
   // deferred (async) render state
   bool pending = false;
   hipStream_t pending_stream = nullptr;
   uint64_t pending_samples = 0;
+  bool pending_tile_order = false;
 };
 
 extern "C" {
@@ -1225,6 +1234,7 @@ void rtg_scene_destroy(rtg_scene* s) {
   if (s->host_counters) (void)hipHostFree(s->host_counters);
   if (s->host_stage) (void)hipHostFree(s->host_stage);
   if (s->dev_out) (void)hipFree(s->dev_out);
+  if (s->order_dev) (void)hipFree(s->order_dev);
   for (ScratchBuf* b : {&s->scr_spill, &s->scr_trace, &s->scr_partial})
     if (b->p) (void)hipFree(b->p);
   if (s->ev0) (void)hipEventDestroy(s->ev0);
@@ -1256,6 +1266,8 @@ static rtg_status collect_stats(rtg_scene* s, rtg_render_stats* stats) {
     stats->kernel_ms = ms;
     for (int k = 0; k < 16; ++k) stats->diag[k] = c[8 + k];
     stats->stack_spills = c[26];
+    stats->tile_order = s->pending_tile_order ? 1u : 0u;
+    stats->tile_order_tune_us = static_cast<uint32_t>(std::min(s->order_tune_ms * 1e3, 4e9));
   }
   // stats stay filled for diagnosis; the frame is not valid in either case
   if (c[4] != 0)
@@ -1294,6 +1306,18 @@ struct Plan {
   size_t out_bytes = 0;
   KernelChoice kmain, kaux;
 };
+
+uint64_t treelet_key(const rtg_camera_desc* c, const rtg_render_desc* j);
+
+// The camera and shard tiles a tile order was tuned for: the treelet key (camera, width, first row, row
+// stride) and the plan's tile layout (rows, tile width, tiles), so a row_count of 0 and the shard's row
+// count name the same order.
+uint64_t order_key(const rtg_camera_desc* c, const rtg_render_desc* j, const DevJob& dj) {
+  uint64_t h = treelet_key(c, j);
+  for (const int64_t v : {int64_t(dj.row_count), int64_t(dj.tile_lw), int64_t(dj.tiles_x), int64_t(dj.num_tiles)})
+    h = (h ^ static_cast<uint64_t>(v)) * 1099511628211ull;
+  return h | 1;  // never 0 (0: not tuned)
+}
 
 rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, Plan* P) {
   if (!s || !cam || !job) return fail(RTG_E_INVALID, "null argument");
@@ -1527,6 +1551,13 @@ rtg_status plan_render(const rtg_scene* s, const rtg_camera_desc* cam, const rtg
     P->ring_slots = 1 << lg;
     P->ring_bytes = (static_cast<size_t>(dj.chunks) << (lg + 10)) + (size_t(8) << lg);
   }
+  // the tile hand-out order rtg_scene_prepare tuned for this camera and shard (none for the ring kernels, whose
+  // slot hand-off needs tile-major order); the tile-cost probe's counters in its own (counting) render
+  dj.tile_order = variant == 3 && dj.ring_log2 < 0 && s->order_dev && s->order_tiles == dj.num_tiles &&
+                          s->order_key == order_key(cam, job, dj)
+                      ? s->order_dev
+                      : nullptr;
+  dj.tile_cost = P->count ? s->probe_tile_cost : nullptr;
   // max_depth <= 0: every pixel is black and nothing is traced (camera.hpp:183-186): no kernel; the frame
   // (one-shot) or the chunk sums (progressive) are zeroed by rtg_render
   P->skip_kernel = dc.max_depth <= 0;
@@ -1673,6 +1704,83 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
   return RTG_OK;
 }
 
+// Cost-ordered tile hand-out (round 6; DESIGN.md §3 "tile order"). Units are handed out tile-major, so a tile
+// of expensive pixels (the earth's contact with the ground in config 3, glass in book-1) may start late and
+// run past the rest of the launch: the wave timeline of an 8-GPU shard of config 3 ends 2 ms after its median
+// wave. A probe render of this camera and shard (the counting kernel at up to 4 samples per pixel, one counter
+// per tile: the segments its units traced) ranks the tiles; renders of that camera and shard then hand out
+// the tiles in descending cost (ties in tile order), so the expensive units start first and the launch ends
+// on cheap ones. Which wave renders a unit, and when, changes; what each unit sums does not: frames and
+// segment counts are identical. For the LDS-resident schedule (3) only: the treelet schedule reads nodes and
+// primitives through L1/L2, where tile-major order keeps the waves of a CU on neighbouring pixels — ordered by
+// cost, config 5 rendered 3 % slower at N = 1 and 11 % slower per 8-GPU shard (profiles/r06_q). Nor for the
+// ring kernels (their slot hand-off needs tile-major order).
+bool wants_tile_order(const rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, const Plan& P) {
+  return s->knobs.tile_order && !P.count && P.variant == 3 && !P.skip_kernel && P.dj.ring_log2 < 0 &&
+         P.dj.num_tiles > 1 && order_key(cam, job, P.dj) != s->order_key;
+}
+
+rtg_status tune_tile_order(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render_desc* job, const Plan& P) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int64_t n = P.dj.num_tiles;
+  const uint64_t key = order_key(cam, job, P.dj);
+  s->order_key = 0;  // the previous order no longer holds while this one is built
+  rtg_camera_desc c2 = *cam;
+  c2.samples_per_pixel = std::min(cam->samples_per_pixel, 4);
+  rtg_render_desc j2 = *job;
+  j2.flags = RTG_RENDER_COUNT | RTG_RENDER_OUT_DEVICE | (job->flags & (0xff << 8));  // the render's schedule
+  j2.row_count = P.rows;
+  j2.partial = nullptr;
+  j2.chunk_begin = j2.chunk_count = 0;
+  j2.stream = nullptr;
+  uint32_t* cost = nullptr;
+  float* out = nullptr;
+  RTG_HIP(dev_alloc(reinterpret_cast<void**>(&cost), n * 4), "hipMalloc(tile costs)");
+  hipError_t e = dev_alloc(reinterpret_cast<void**>(&out), int64_t(P.rows) * P.W * 12);
+  hipStream_t os = s->own_stream;  // the probe runs on the scene's own stream: every copy here is ordered on it
+  if (e == hipSuccess) e = hipMemsetAsync(cost, 0, n * 4, os);
+  rtg_status st = e == hipSuccess ? RTG_OK : hip_fail(e, "tile-cost probe buffers");
+  if (st == RTG_OK) {
+    s->probe_tile_cost = cost;
+    rtg_render_stats ps{};
+    st = rtg_render(s, &c2, &j2, out, &ps);
+    s->probe_tile_cost = nullptr;
+  }
+  std::vector<uint32_t> cnt;
+  if (st == RTG_OK) {
+    cnt.resize(n);
+    e = hipMemcpyAsync(cnt.data(), cost, n * 4, hipMemcpyDeviceToHost, os);
+    if (e == hipSuccess) e = hipStreamSynchronize(os);
+    if (e != hipSuccess) st = hip_fail(e, "tile-cost download");
+  }
+  (void)hipFree(out);
+  (void)hipFree(cost);
+  if (st != RTG_OK) return st;
+  std::vector<int32_t> order(n);
+  for (int64_t k = 0; k < n; ++k) order[k] = static_cast<int32_t>(k);
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return cnt[a] > cnt[b]; });
+  if (s->order_cap < n) {
+    if (s->order_dev) RTG_HIP(hipFree(s->order_dev), "hipFree(tile order)");  // device-synchronous
+    s->order_dev = nullptr;
+    s->order_cap = 0;
+    RTG_HIP(dev_alloc(reinterpret_cast<void**>(&s->order_dev), n * 4), "hipMalloc(tile order)");
+    s->order_cap = n;
+  }
+  RTG_HIP(hipMemcpyAsync(s->order_dev, order.data(), n * 4, hipMemcpyHostToDevice, os), "tile order upload");
+  RTG_HIP(hipStreamSynchronize(os), "tile order upload");
+  s->order_tiles = n;
+  s->order_key = key;
+  s->order_tune_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (s->knobs.verbose) {
+    uint64_t total = 0;
+    for (const uint32_t c : cnt) total += c;
+    std::fprintf(stderr, "[rtg] tile order: %.1f ms, %lld tiles, probe %d spp, %llu segments, costliest tile %u\n",
+                 s->order_tune_ms, static_cast<long long>(n), c2.samples_per_pixel,
+                 static_cast<unsigned long long>(total), n ? cnt[order[0]] : 0u);
+  }
+  return RTG_OK;
+}
+
 // The culling margin covers ray origins with |coordinate| <= 2 s->origin_bound (culling_box: M = the
 // primitive boxes' reach when the scene was created). A camera whose lens reaches farther out widens every
 // node box on the device first (repad_nodes_kernel, on the render's stream; 1/16 headroom so a camera moving
@@ -1761,13 +1869,19 @@ rtg_status rtg_scene_prepare(rtg_scene* s, const rtg_camera_desc* cam, const rtg
   if (!s || !cam || !job) return fail(RTG_E_INVALID, "null argument");
   if (s->pending) return fail(RTG_E_INVALID, "a previous async render was not waited for");
   Plan P;
-  const rtg_status pst = plan_render(s, cam, job, &P);
+  rtg_status pst = plan_render(s, cam, job, &P);
   if (pst != RTG_OK) return pst;
-  if (!wants_treelet_tune(s, cam, job, P)) return RTG_OK;
+  const bool treelet = wants_treelet_tune(s, cam, job, P), order = wants_tile_order(s, cam, job, P);
+  if (!treelet && !order) return RTG_OK;
   RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
-  // renders still in flight on the caller's stream read the node array this renumbers
+  // renders still in flight on the caller's stream read the node array and the tile order this rewrites
   if (job->stream) RTG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(job->stream)), "stream sync");
-  return tune_treelet(s, cam, job, treelet_key(cam, job));
+  if (treelet) {
+    pst = tune_treelet(s, cam, job, treelet_key(cam, job));
+    if (pst != RTG_OK) return pst;
+  }
+  // the tile order's probe runs on the renumbered node array (same frames; its costs are the render's)
+  return order ? tune_tile_order(s, cam, job, P) : RTG_OK;
 }
 
 rtg_status rtg_hot_treelet_order_host(int32_t* nodes, const uint32_t* visits, int64_t num_nodes) {
@@ -1797,7 +1911,10 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
   // plan again); a later camera or shard re-tunes only through rtg_scene_prepare, so a moving camera does
   // not pay a probe render and a node re-upload inside every frame's rtg_render
   if (s->treelet_key == 0 && wants_treelet_tune(s, cam, job, P)) {
-    pst = rtg_scene_prepare(s, cam, job);
+    // the hot treelet only: the tile order's probe is rtg_scene_prepare's (no second probe inside a render)
+    RTG_HIP(hipSetDevice(s->device), "hipSetDevice");
+    if (job->stream) RTG_HIP(hipStreamSynchronize(static_cast<hipStream_t>(job->stream)), "stream sync");
+    pst = tune_treelet(s, cam, job, treelet_key(cam, job));
     if (pst != RTG_OK) return pst;
     P = Plan{};
     pst = plan_render(s, cam, job, &P);
@@ -1944,6 +2061,7 @@ rtg_status rtg_render(rtg_scene* s, const rtg_camera_desc* cam, const rtg_render
     const int s1 = P.progressive ? std::min(spp, (dj.chunk_begin + dj.chunks) * dj.chunk_samples) : spp;
     s->pending_samples = static_cast<uint64_t>(rows) * W * static_cast<uint64_t>(s1 - s0);
   }
+  s->pending_tile_order = dj.tile_order != nullptr;
   if (P.async) return RTG_OK;
   return collect_stats(s, stats);
 }

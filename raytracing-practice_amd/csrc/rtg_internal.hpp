@@ -259,6 +259,8 @@ struct Knobs {
                                 // (fewer: more treelet nodes, more spill traffic; spilling trees only)
   int treelet_hot = 1;          // RTG_TREELET_HOT 0 | 1: treelet of the most-visited nodes for the
                                 // camera (a probe render counts node visits), 0: breadth-first top
+  int tile_order = 1;           // RTG_TILE_ORDER 0 | 1: rtg_scene_prepare orders the tile hand-out by a
+                                // probe render's per-tile cost (1), or leaves it tile-major (0)
   std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
 };
 Knobs read_knobs();
@@ -308,6 +310,11 @@ struct DevJob {
   int32_t stack_esz;                         // persistent kernels: bytes per LDS stack entry (2 or 4)
   int32_t lds_stacks;                        // persistent kernels: byte offset of the traversal stacks in LDS
   int32_t lds_ring;                          // RING kernels: byte offset of the per-wave batch tables (64 B each)
+  // cost-ordered hand-out (rtg_scene_prepare): the tile handed out at each position, num_tiles entries, the
+  // probe's most expensive tile first; null: tile-major (always null for RING kernels)
+  const int32_t* tile_order;
+  // the tile-cost probe (COUNT kernels only): segments traced per tile, num_tiles counters; else null
+  uint32_t* tile_cost;
 };
 
 }  // namespace rtg

@@ -315,6 +315,29 @@ __device__ __forceinline__ const int32_t* tie_ranks_at_tie(const DevScene& S, bo
   }
   return r;
 }
+// DevJob::tile_order read from the kernel arguments where a batch is handed out, as tie_ranks_late reads the
+// tie ranks: J.tile_order itself was held in SGPRs from the kernel's start and pushed other scalars into VGPR
+// lanes (config 2 +1 % with the order off). Every kernel that runs render_stream takes (DevScene, DevCamera,
+// DevJob) by value, so DevJob sits at the offset below in the kernel-argument segment (arguments in order, each
+// at its own alignment); the COUNT kernels compare the two pointers and report a mismatch as corrupt.
+constexpr size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+constexpr size_t kDevJobKernarg =
+    align_up(align_up(sizeof(DevScene), alignof(DevCamera)) + sizeof(DevCamera), alignof(DevJob));
+template <bool COUNT>
+__device__ __forceinline__ const int32_t* tile_order_late(const DevJob& J, bool& corrupt) {
+  const char* ka = (const char*)(__builtin_amdgcn_kernarg_segment_ptr());
+  const uint64_t v = reinterpret_cast<uint64_t>(
+      *reinterpret_cast<const int32_t* const volatile*>(ka + kDevJobKernarg + offsetof(DevJob, tile_order)));
+  // the load is a vector load: its (uniform) value back into SGPRs, so the null test is a scalar branch
+  const int32_t* r = reinterpret_cast<const int32_t*>(
+      (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v >> 32)))) << 32) |
+      static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(v & 0xffffffffu))));
+  if (COUNT && r != J.tile_order) {
+    corrupt = true;
+    return J.tile_order;
+  }
+  return r;
+}
 // Cache-read schedules (Trav::mat holds the hit's material): the closest hit's rank is re-read from the
 // list ranks, only on a tie (wave-uniform branch).
 __device__ __forceinline__ bool quad_wins_tie(const DevScene& S, int32_t qrank, int32_t best) {
@@ -1248,6 +1271,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
   // kernels had none to spare; the host keeps spp < 2^26 and K <= 63)
   constexpr uint32_t kSampleBits = 26, kSampleMask = (1u << kSampleBits) - 1u;
   uint32_t su = 0;
+  uint32_t seg0 = 0;  // COUNT: the lane's segment count when its unit started (the tile-cost probe)
   int chunk = 0;
   auto has = [&]() { return su != 0; };
   // fresh: the lane starts sample (su & kSampleMask) of its unit at the top of the next loop trip (the one
@@ -1321,8 +1345,16 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           exhausted = true;
           break;
         }
-        const int tile = b / J.chunks;
-        bc = J.chunk_begin + (b - tile * J.chunks);
+        const int tpos = b / J.chunks;  // the batch's tile position in the hand-out order
+        bc = J.chunk_begin + (b - tpos * J.chunks);
+        // cost-ordered hand-out (rtg_scene_prepare's tile order): the tile at that position, the
+        // most expensive first; tile-major without one, and always in the ring kernels (their slot hand-off
+        // needs tile-major order). Only when a unit is rendered changes, never what it sums: frames identical
+        int tile = tpos;
+        if constexpr (!RING) {
+          const int32_t* order = tile_order_late<COUNT>(J, w.corrupt);
+          if (order != nullptr) tile = __builtin_amdgcn_readfirstlane(order[tpos]);  // wave-uniform: SALU below
+        }
         const int ty = tile / J.tiles_x;
         bx = (tile - ty * J.tiles_x) << J.tile_lw;
         by = ty << (6 - J.tile_lw);
@@ -1353,6 +1385,7 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           chunk = ring ? ((((cur_tile() & ((1 << J.ring_log2) - 1)) * J.chunks + (bc - J.chunk_begin)) << 6) + k) |
                              (cur_e << 28)
                        : bc;
+          if (COUNT) seg0 = w.segs;  // the tile-cost probe: this unit's segments are counted from here
           const int s0 = bc * J.chunk_samples;
           su = (static_cast<uint32_t>(min(s0 + J.chunk_samples, C.spp) - s0) << kSampleBits) | static_cast<uint32_t>(s0);
           acc = v3(0.0f, 0.0f, 0.0f);
@@ -1499,6 +1532,9 @@ __device__ __forceinline__ void render_stream(const DevScene& S, const DevCamera
           }
           su = 0;  // the unit is done
           ++w.pixels;
+          // the tile-cost probe (rtg_scene_prepare): the unit's segments into its tile's counter
+          if (COUNT && J.tile_cost != nullptr)
+            atomicAdd(J.tile_cost + (px_lr(px) >> (6 - J.tile_lw)) * J.tiles_x + (px_i(px) >> J.tile_lw), w.segs - seg0);
         }
       }
       if (COUNT) w.diag[12] += __builtin_amdgcn_s_memtime() - t_end;

@@ -102,7 +102,8 @@ class rtg_render_desc(C.Structure):
 class rtg_render_stats(C.Structure):
     _fields_ = [("segments", C.c_uint64), ("samples", C.c_uint64), ("box_tests", C.c_uint64),
                 ("prim_tests", C.c_uint64), ("hits", C.c_uint64), ("kernel_ms", C.c_double),
-                ("diag", C.c_uint64 * 16), ("stack_spills", C.c_uint64), ("reserved_", C.c_uint64 * 3)]
+                ("diag", C.c_uint64 * 16), ("stack_spills", C.c_uint64), ("tile_order", C.c_uint32),
+                ("tile_order_tune_us", C.c_uint32), ("reserved_", C.c_uint64 * 2)]
 
 
 class rtg_scene_info(C.Structure):

@@ -321,6 +321,78 @@ def test_hot_treelet_keeps_the_frame(gpu_lib, scenes, oracle, monkeypatch):
     assert pb.schedule == 3 and pb.treelet_hot == 0 and pb.treelet_tune_us == 0
 
 
+def test_tile_order_keeps_the_frame(gpu_lib, scenes, oracle, monkeypatch):
+    """Cost-ordered tile hand-out (rtg_scene_prepare, DESIGN.md §3 "tile order"): a probe render counts each
+    tile's segments for the camera and shard, and later renders of that camera and shard hand the tiles out
+    most expensive first. Only when a unit is rendered changes: frames and segment counts equal the tile-major
+    render's, bit for bit, on book-1 (LDS schedule, two sample chunks), a strided shard of it and Cornell (five
+    4-wave workgroups); another camera or shard, the treelet schedule (1M spheres), the tile-ring kernels and
+    RTG_TILE_ORDER=0 keep tile-major order."""
+    b = scenes.build("bouncing_spheres", grid=11, rand_seed=1)
+    c = rtgpu.rtg_camera_desc.from_buffer_copy(b.camera)
+    c.image_width, c.samples_per_pixel, c.max_depth = 192, 32, 50
+    ds = gpu_lib.scene_create(b.desc)
+    f0, st0 = ds.render_host(c)
+    assert st0.tile_order == 0
+    ds.prepare(c)
+    f1, st1 = ds.render_host(c)
+    assert st1.tile_order == 1 and st1.tile_order_tune_us > 0
+    assert np.array_equal(f1, f0) and st1.segments == st0.segments
+    o, segs = oracle.render_f32(b.desc, c)
+    assert_parity(f1, o, st1, segs)
+    # the counting kernel reads the order where the product kernels do (from the kernel arguments) and
+    # reports a mismatch with its DevJob as a corrupt render
+    _, cst = ds.render_host(c, count=True)
+    assert cst.tile_order == 1 and cst.segments == st0.segments
+    # a strided shard is another tile layout: tile-major until prepared for it, then ordered, same rows
+    s0, sst0 = ds.render_host(c, row_begin=1, row_stride=3)
+    assert sst0.tile_order == 0
+    ds.prepare(c, row_begin=1, row_stride=3)
+    s1, sst1 = ds.render_host(c, row_begin=1, row_stride=3)
+    assert sst1.tile_order == 1 and np.array_equal(s1, s0) and sst1.segments == sst0.segments
+    assert np.array_equal(s1, f0[1::3])
+    _, st2 = ds.render_host(c)  # the scene keeps one order: the full frame's was replaced
+    assert st2.tile_order == 0
+    # the tile-ring kernels keep tile-major order (their slot hand-off needs it)
+    ds.close()
+    monkeypatch.setenv("RTG_TILE_SLOTS", "8")
+    dr = gpu_lib.scene_create(b.desc)
+    monkeypatch.delenv("RTG_TILE_SLOTS")
+    dr.prepare(c)
+    fr, str_ = dr.render_host(c)
+    dr.close()
+    assert str_.tile_order == 0 and np.array_equal(fr, f0)
+    monkeypatch.setenv("RTG_TILE_ORDER", "0")
+    dk = gpu_lib.scene_create(b.desc)
+    monkeypatch.delenv("RTG_TILE_ORDER")
+    dk.prepare(c)
+    fk, stk = dk.render_host(c)
+    dk.close()
+    assert stk.tile_order == 0 and np.array_equal(fk, f0)
+    # the treelet schedule reads nodes and primitives through the caches, where tile-major order keeps a CU's
+    # waves on neighbouring pixels: rtg_scene_prepare tunes its hot treelet and leaves the hand-out alone
+    g = scenes.build("bouncing_spheres", grid=500, rand_seed=1)
+    cg = rtgpu.rtg_camera_desc.from_buffer_copy(g.camera)
+    cg.image_width, cg.aspect_ratio, cg.samples_per_pixel, cg.max_depth = 160, 16.0 / 9.0, 20, 50
+    dg = gpu_lib.scene_create(g.desc)
+    g0, gst0 = dg.render_host(cg)  # the first render tunes the hot treelet only
+    assert gst0.tile_order == 0 and dg.plan(cg).treelet_hot == 1
+    dg.prepare(cg)
+    g1, gst1 = dg.render_host(cg)
+    dg.close()
+    assert gst1.tile_order == 0 and np.array_equal(g1, g0) and gst1.segments == gst0.segments
+    # Cornell: five 4-wave workgroups per CU
+    k = scenes.build("cornell_box", rand_seed=1)
+    ck = rtgpu.rtg_camera_desc.from_buffer_copy(k.camera)
+    ck.image_width, ck.samples_per_pixel, ck.max_depth = 96, 24, 100
+    dc = gpu_lib.scene_create(k.desc)
+    k0, kst0 = dc.render_host(ck)
+    dc.prepare(ck)
+    k1, kst1 = dc.render_host(ck)
+    dc.close()
+    assert kst1.tile_order == 1 and np.array_equal(k1, k0) and kst1.segments == kst0.segments
+
+
 def test_repeated_host_renders_are_identical(gpu_lib, scenes):
     """Host-output renders go through a scene-owned device frame and a pinned staging buffer; with
     a stream-ordered (hipMallocAsync) frame the third render of a scene came back all zero."""

@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--count", action="store_true", help="also report box / prim tests per segment per variant")
     ap.add_argument("--height", type=int, default=0, help="0: 16:9 of --width")
+    ap.add_argument("--prepare", action="store_true",
+                    help="rtg_scene_prepare each scene for the camera before the rounds (hot treelet, tile order)")
     a = ap.parse_args()
     import torch
 
@@ -65,6 +67,8 @@ def main():
                 os.environ.pop("RTG_SAH_TUNE", None)
             scenes[(name, tune, env)] = libs[name].scene_create(s.desc)
             os.environ.pop("RTG_SAH_TUNE", None)
+            if a.prepare:
+                scenes[(name, tune, env)].prepare(cam)
         return scenes[(name, tune, env)]
     out = torch.zeros((H, a.width, 3), device="cuda")
     stream = torch.cuda.current_stream().cuda_stream

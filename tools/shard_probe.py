@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--lib", default="", help="librtgpu.so to load (default: the in-tree build)")
+    ap.add_argument("--prepare", action="store_true",
+                    help="rtg_scene_prepare each shard before its renders (hot treelet, tile order), as bench.py does")
     ap.add_argument("--layout", default="strided", choices=["strided", "contig"],
                     help="contig: rank r renders one block of ceil(H/N) rows (coherence probe; unbalanced)")
     a = ap.parse_args()
@@ -58,6 +60,8 @@ def main():
                 kern.append(0.0)
                 wall.append(0.0)
                 continue
+            if a.prepare:
+                ds.prepare(cam, row_begin=b, row_stride=stride, row_count=cnt)
             best_k, best_w = 1e30, 1e30
             for _ in range(a.reps):
                 torch.cuda.synchronize()

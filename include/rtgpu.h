@@ -347,7 +347,7 @@ rtg_status rtg_render_plan(rtg_scene* scene, const rtg_camera_desc* cam, const r
  * called for them: a moving camera pays no probe and node re-upload inside its frames); calling this
  * first keeps the probe (~0.13 s for 1M spheres at 4K) out of that render. A no-op for every other
  * schedule and with RTG_TREELET_HOT=0.
- * Not concurrent with renders of the same scene (it rewrites the scene's node array). No reference
+ * Not concurrent with renders of the same scene (it rewrites the scene's node array and tile order). No reference
  * counterpart: the reference's bvh_node keeps its nodes in host memory (bvh_node.hpp:25-77). */
 rtg_status rtg_scene_prepare(rtg_scene* scene, const rtg_camera_desc* cam, const rtg_render_desc* job);
 

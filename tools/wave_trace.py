@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--schedule", type=int, default=0)
     ap.add_argument("--lib", default=None)
     ap.add_argument("--shard-of", type=int, default=1, help="render rank 0's interleaved shard of N ranks")
+    ap.add_argument("--prepare", action="store_true", help="rtg_scene_prepare the shard first (tile order)")
     a = ap.parse_args()
     import ctypes as C
 
@@ -42,6 +43,8 @@ def main():
     ds = lib.scene_create(s.desc)
     H = lib.camera_resolve(s.camera).image_height
     b, stride, cnt = rtgpu.shard_rows(H, 0, a.shard_of)
+    if a.prepare:
+        ds.prepare(s.camera, row_begin=b, row_stride=stride, row_count=cnt if a.shard_of > 1 else 0)
     buf = np.zeros((max(cnt, 1), a.width, 3), dtype=np.float32)
     job = rtgpu.rtg_render_desc(0x5EED, b, stride, cnt if a.shard_of > 1 else 0, a.schedule << 8, None)
     st = rtgpu.rtg_render_stats()
@@ -56,7 +59,8 @@ def main():
     tick_ns = 10.0  # s_memrealtime runs at 100 MHz
     grid = np.linspace(base, base + span, 11)
     alive = [int(np.sum((t0 <= g) & (t1 > g))) for g in grid[:-1]]
-    out = {"scene": a.scene, "shard_of": a.shard_of, "schedule": a.schedule, "kernel_ms": round(st.kernel_ms, 2), "waves": int(len(t)),
+    out = {"scene": a.scene, "shard_of": a.shard_of, "schedule": a.schedule, "tile_order": int(st.tile_order),
+           "kernel_ms": round(st.kernel_ms, 2), "waves": int(len(t)),
            "span_ms": round(span * tick_ns / 1e6, 2),
            "alive_at_tenths": alive,
            "start_ms_pcts": [round((np.percentile(t0, q) - base) * tick_ns / 1e6, 2) for q in (0, 50, 90, 100)],

@@ -330,6 +330,7 @@ Knobs read_knobs() {
   num("RTG_TREELET_STACK", 4, 16, &k.treelet_stack);
   num("RTG_TREELET_HOT", 0, 1, &k.treelet_hot);
   num("RTG_TILE_ORDER", 0, 1, &k.tile_order);
+  num("RTG_TILE_ORDER_SPP", 1, 64, &k.tile_order_spp);
   if (const char* e = std::getenv("RTG_WAVE_TRACE")) k.wave_trace = e;
   return k;
 }
@@ -1707,7 +1708,8 @@ rtg_status tune_treelet(rtg_scene* s, const rtg_camera_desc* cam, const rtg_rend
 // Cost-ordered tile hand-out (round 6; DESIGN.md §3 "tile order"). Units are handed out tile-major, so a tile
 // of expensive pixels (the earth's contact with the ground in config 3, glass in book-1) may start late and
 // run past the rest of the launch: the wave timeline of an 8-GPU shard of config 3 ends 2 ms after its median
-// wave. A probe render of this camera and shard (the counting kernel at up to 4 samples per pixel, one counter
+// wave. A probe render of this camera and shard (the counting kernel at up to 4 samples per pixel by default,
+// RTG_TILE_ORDER_SPP, one counter
 // per tile: the segments its units traced) ranks the tiles; renders of that camera and shard then hand out
 // the tiles in descending cost (ties in tile order), so the expensive units start first and the launch ends
 // on cheap ones. Which wave renders a unit, and when, changes; what each unit sums does not: frames and
@@ -1726,7 +1728,7 @@ rtg_status tune_tile_order(rtg_scene* s, const rtg_camera_desc* cam, const rtg_r
   const uint64_t key = order_key(cam, job, P.dj);
   s->order_key = 0;  // the previous order no longer holds while this one is built
   rtg_camera_desc c2 = *cam;
-  c2.samples_per_pixel = std::min(cam->samples_per_pixel, 4);
+  c2.samples_per_pixel = std::min(cam->samples_per_pixel, s->knobs.tile_order_spp);
   rtg_render_desc j2 = *job;
   j2.flags = RTG_RENDER_COUNT | RTG_RENDER_OUT_DEVICE | (job->flags & (0xff << 8));  // the render's schedule
   j2.row_count = P.rows;

@@ -261,6 +261,7 @@ struct Knobs {
                                 // camera (a probe render counts node visits), 0: breadth-first top
   int tile_order = 1;           // RTG_TILE_ORDER 0 | 1: rtg_scene_prepare orders the tile hand-out by a
                                 // probe render's per-tile cost (1), or leaves it tile-major (0)
+  int tile_order_spp = 4;       // RTG_TILE_ORDER_SPP 1..64: samples per pixel of that probe (at most the render's)
   std::string wave_trace;      // RTG_WAVE_TRACE=<file>: per-wave timeline (tools/wave_trace.py)
 };
 Knobs read_knobs();

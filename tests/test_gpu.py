@@ -579,9 +579,11 @@ def test_progressive_chunks_and_checkpoint(gpu_lib, scenes):
     saved = partial.cpu()  # checkpoint
     ds.close()
     ds = gpu_lib.scene_create(s.desc)
+    ds.prepare(c)  # the resumed chunks in the prepared tile order: the same sums
     resumed = saved.cuda()
-    ds.render_chunks(c, resumed.data_ptr(), 3, 0, out.data_ptr(), stream, seed=7)
+    st = ds.render_chunks(c, resumed.data_ptr(), 3, 0, out.data_ptr(), stream, seed=7)
     torch.cuda.synchronize()
+    assert st.tile_order == 1
     assert np.array_equal(out.cpu().numpy(), full)
     assert np.array_equal(resumed[:3].cpu().numpy(), saved[:3].numpy())  # finished chunks untouched
     ds.close()

@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--block", type=int, default=32)
     ap.add_argument("--rows-from", type=int, default=0)
     ap.add_argument("--rows-to", type=int, default=-1)
+    ap.add_argument("--prepare", action="store_true",
+                    help="rtg_scene_prepare the camera first (hot treelet, tile order), as bench.py does")
     a = ap.parse_args()
     import rtgpu
     from oracle_bind import Oracle
@@ -44,8 +46,11 @@ def main():
                                    spp=a.spp, max_depth=a.depth)
     cam = s.camera
     ds = lib.scene_create(s.desc)
+    if a.prepare:
+        ds.prepare(cam)
     t0 = time.time()
     gpu, st = ds.render_host(cam)
+    tile_order = int(st.tile_order)
     ds.close()
     H = gpu.shape[0]
     tie_rule = None
@@ -81,7 +86,7 @@ def main():
            "rmse": float(np.sqrt(np.mean((g.astype(np.float64) - ref) ** 2))),
            "max_abs": float(np.max(np.abs(g.astype(np.float64) - ref))) if g.size else 0.0,
            "oracle_segments": int(segs),
-           "gpu_segments_whole_frame": int(st.segments),
+           "gpu_segments_whole_frame": int(st.segments), "gpu_tile_order": tile_order,
            "oracle_seconds": round(time.time() - t0, 1), "threads": a.threads,
            "differing": [[int(x), int(y) + a.rows_from] for y, x in zip(ys[:64], xs[:64])]}
     if tie_rule is not None:
